@@ -1,0 +1,134 @@
+/*
+ * s3dlio_gpu.h — C ABI of the MI355X-native synthetic object-payload
+ * generator (drop-in for s3dlio's src/data_gen.rs hot path).
+ *
+ * Every entry point is plain C: pointers, sizes, integers.  All functions
+ * return 0 on success or a negative S3DG_E* code; s3dg_last_error() returns
+ * a thread-local message for the last failure on the calling thread.
+ *
+ * Reference interfaces replaced (paths relative to the s3dlio checkout):
+ *   s3dlio_fill_controlled_data         src/data_gen.rs:151  fill_controlled_data(buf,dedup,compress)
+ *   s3dlio_fill_controlled_data_seeded  src/data_gen.rs:151  (seeded sibling)
+ *   s3dg_fill_controlled                src/data_gen.rs:198-223 (the Rayon par_chunks_mut loop)
+ *   s3dg_fill_controlled_stream         src/s3_utils.rs:1741 / src/bin/cli.rs:2282 generate_object
+ *                                       fan-out, one payload per object
+ *   s3dg_fill_controlled_batch          same, mixed object sizes (BASELINE config 4)
+ *   s3dg_unique_blocks                  src/data_gen.rs:162-167
+ *   s3dg_compress_ratio                 src/data_gen.rs:169-173
+ *
+ * Device pointers passed to s3dg_fill_* must be 16-byte aligned (objects in
+ * a stream/batch too); `stream` is a hipStream_t (NULL = legacy default).
+ */
+#ifndef S3DLIO_GPU_H
+#define S3DLIO_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#pragma GCC visibility push(default)
+
+#define S3DG_BLOCK_SIZE 4096u   /* BLK_SIZE, src/constants.rs:326 */
+
+enum {
+    S3DG_OK = 0,
+    S3DG_EINVAL = -1,   /* bad argument (null, misaligned, out of range) */
+    S3DG_EHIP = -2,     /* HIP runtime error (message in s3dg_last_error) */
+    S3DG_ENOMEM = -3,
+};
+
+typedef struct s3dg_ctx s3dg_ctx;
+
+/* One object of a batch: `dst_off` bytes from dst_base (multiple of 16),
+ * `size` bytes, block seeds `u + entropy` (src/data_gen.rs:202), zero-prefix
+ * ratio f_num/f_den of each 4 KiB block (compress c -> (c-1, c)). */
+typedef struct {
+    uint64_t dst_off;
+    uint64_t size;
+    uint64_t entropy;
+    uint64_t dedup;
+    uint32_t f_num;
+    uint32_t f_den;
+} s3dg_obj_desc;
+
+/* ---- context ------------------------------------------------------------ */
+int s3dg_ctx_create(int device, s3dg_ctx **out);
+int s3dg_ctx_destroy(s3dg_ctx *ctx);
+/* Replace the 4 KiB base block (stands in for A_BASE_BLOCK,
+ * src/constants.rs:715-720).  Host pointer, 4096 bytes. */
+int s3dg_set_base_block(s3dg_ctx *ctx, const uint8_t *base4096);
+/* Base block = Xoshiro256++(seed_from_u64(seed)).fill_bytes(4096). */
+int s3dg_set_base_block_seed(s3dg_ctx *ctx, uint64_t seed);
+int s3dg_get_base_block(s3dg_ctx *ctx, uint8_t *out4096);
+/* Workgroups per CU of the persistent launch (default 4; 0 = default). */
+int s3dg_set_occupancy(s3dg_ctx *ctx, int wg_per_cu);
+/* 1 = nontemporal stores (default), 0 = plain stores. */
+int s3dg_set_nontemporal(s3dg_ctx *ctx, int on);
+
+/* ---- parameter helpers (host math shared with the kernels) --------------- */
+uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup);
+int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
+/* Per-object entropy of object j of a stream: seed_base + j * 2^32. */
+uint64_t s3dg_object_entropy(uint64_t seed_base, uint64_t j);
+
+/* ---- device-resident generation (asynchronous on `stream`) -------------- */
+/* One object of `len` bytes at dst (device). */
+int s3dg_fill_controlled(s3dg_ctx *ctx, void *dst, uint64_t len, uint64_t dedup,
+                         uint32_t f_num, uint32_t f_den, uint64_t entropy,
+                         void *stream);
+/* Blocks [blk_lo, blk_hi) of one `len`-byte object: block blk_lo lands at
+ * dst.  Used to stream one large object through a smaller device buffer. */
+int s3dg_fill_controlled_range(s3dg_ctx *ctx, void *dst, uint64_t len,
+                               uint64_t blk_lo, uint64_t blk_hi, uint64_t dedup,
+                               uint32_t f_num, uint32_t f_den, uint64_t entropy,
+                               void *stream);
+/* n equal-size objects, object j at dst + j*stride, entropy
+ * s3dg_object_entropy(seed_base, first_obj + j). */
+int s3dg_fill_controlled_stream(s3dg_ctx *ctx, void *dst, uint64_t obj_size,
+                                uint64_t stride, uint64_t n_objs, uint64_t dedup,
+                                uint32_t f_num, uint32_t f_den, uint64_t seed_base,
+                                uint64_t first_obj, void *stream);
+/* Mixed-size batch.  `descs` is a host array; it is copied before return. */
+int s3dg_fill_controlled_batch(s3dg_ctx *ctx, void *dst_base,
+                               const s3dg_obj_desc *descs, uint64_t n, void *stream);
+/* Write-only ceiling: fill `len` bytes with a constant using the same store
+ * path (roofline denominator measured on the device). */
+int s3dg_write_ceiling(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern,
+                       void *stream);
+
+/* ---- memory / copy helpers ------------------------------------------------ */
+int s3dg_device_alloc(s3dg_ctx *ctx, uint64_t bytes, void **out);
+int s3dg_device_free(s3dg_ctx *ctx, void *p);
+int s3dg_host_alloc_pinned(uint64_t bytes, void **out);
+int s3dg_host_free_pinned(void *p);
+int s3dg_d2h_async(s3dg_ctx *ctx, void *host, const void *dev, uint64_t len, void *stream);
+int s3dg_h2d_async(s3dg_ctx *ctx, void *dev, const void *host, uint64_t len, void *stream);
+int s3dg_stream_create(s3dg_ctx *ctx, void **out);
+int s3dg_stream_destroy(s3dg_ctx *ctx, void *stream);
+int s3dg_sync(s3dg_ctx *ctx, void *stream);   /* stream NULL: whole device */
+int s3dg_device_count(int *out);
+
+/* ---- host-buffer drop-ins (src/data_gen.rs:151 signature) ---------------- */
+/* fill_controlled_data(buf, dedup, compress): time-based entropy and a
+ * per-process random base block, exactly as the reference; generated on the
+ * GPU of the process-default context (env S3DLIO_GPU_DEVICE, default 0) and
+ * copied into `buf`.  Empty buffer: no-op. */
+int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress);
+/* Seeded sibling: entropy replaces call_entropy; base4096 (nullable)
+ * replaces A_BASE_BLOCK (NULL = the default context's base block). */
+int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup,
+                                       size_t compress, uint64_t entropy,
+                                       const uint8_t *base4096);
+
+const char *s3dg_last_error(void);
+const char *s3dg_version(void);
+
+#pragma GCC visibility pop
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S3DLIO_GPU_H */

@@ -1,0 +1,13 @@
+"""s3dlio_amd — MI355X-native synthetic object-payload generator.
+
+Drop-in for s3dlio's data-generation hot path (src/data_gen.rs), built as
+hand-written gfx950 HIP kernels behind a C ABI (include/s3dlio_gpu.h,
+libs3dlio_amd.so).  Importing this package loads the library; it raises if
+the library is absent (no CPU fallback exists).
+"""
+from ._lib import S3dgError, lib  # noqa: F401  (loads libs3dlio_amd.so)
+from .device import (BLOCK_SIZE, DEFAULT_BASE_SEED, Context, compress_ratio,  # noqa: F401
+                     device_count, object_entropy, unique_blocks)
+from .data_gen import fill_controlled_data, fill_controlled_data_seeded  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,103 @@
+"""ctypes binding of libs3dlio_amd.so (the C ABI in include/s3dlio_gpu.h).
+
+The library is built in-tree by s3dlio_amd/build.py.  There is no fallback:
+if the .so is missing or cannot be loaded, importing this module raises.
+
+HIP runtime: PyTorch-ROCm ships its own libamdhip64.so.7 (same SONAME as
+/opt/rocm's).  When torch is importable we import it first so the dynamic
+loader binds our library to torch's already-loaded runtime and the process
+holds exactly one HIP runtime — then torch streams/events/tensors and this
+library share devices, streams and pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # one HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the product
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libs3dlio_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `python -m s3dlio_amd.build` "
+        "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+
+_L = ctypes.CDLL(LIB_PATH)
+
+c_u64, c_u32, c_int, c_vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class ObjDesc(ctypes.Structure):
+    """s3dg_obj_desc"""
+    _fields_ = [("dst_off", c_u64), ("size", c_u64), ("entropy", c_u64), ("dedup", c_u64),
+                ("f_num", c_u32), ("f_den", c_u32)]
+
+
+# name -> (restype, argtypes); the exact export list of include/s3dlio_gpu.h
+SIGNATURES = {
+    "s3dg_ctx_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
+    "s3dg_ctx_destroy": (c_int, [c_vp]),
+    "s3dg_set_base_block": (c_int, [c_vp, c_u8p]),
+    "s3dg_set_base_block_seed": (c_int, [c_vp, c_u64]),
+    "s3dg_get_base_block": (c_int, [c_vp, c_u8p]),
+    "s3dg_set_occupancy": (c_int, [c_vp, c_int]),
+    "s3dg_set_nontemporal": (c_int, [c_vp, c_int]),
+    "s3dg_unique_blocks": (c_u64, [c_u64, c_u64]),
+    "s3dg_compress_ratio": (c_int, [c_u64, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]),
+    "s3dg_object_entropy": (c_u64, [c_u64, c_u64]),
+    "s3dg_fill_controlled": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),
+    "s3dg_fill_controlled_range": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32,
+                                           c_u64, c_vp]),
+    "s3dg_fill_controlled_stream": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32,
+                                            c_u64, c_u64, c_vp]),
+    "s3dg_fill_controlled_batch": (c_int, [c_vp, c_vp, ctypes.POINTER(ObjDesc), c_u64, c_vp]),
+    "s3dg_write_ceiling": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
+    "s3dg_device_alloc": (c_int, [c_vp, c_u64, ctypes.POINTER(c_vp)]),
+    "s3dg_device_free": (c_int, [c_vp, c_vp]),
+    "s3dg_host_alloc_pinned": (c_int, [c_u64, ctypes.POINTER(c_vp)]),
+    "s3dg_host_free_pinned": (c_int, [c_vp]),
+    "s3dg_d2h_async": (c_int, [c_vp, c_vp, c_vp, c_u64, c_vp]),
+    "s3dg_h2d_async": (c_int, [c_vp, c_vp, c_vp, c_u64, c_vp]),
+    "s3dg_stream_create": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
+    "s3dg_stream_destroy": (c_int, [c_vp, c_vp]),
+    "s3dg_sync": (c_int, [c_vp, c_vp]),
+    "s3dg_device_count": (c_int, [ctypes.POINTER(c_int)]),
+    "s3dlio_fill_controlled_data": (c_int, [c_vp, ctypes.c_size_t, ctypes.c_size_t,
+                                            ctypes.c_size_t]),
+    "s3dlio_fill_controlled_data_seeded": (c_int, [c_vp, ctypes.c_size_t, ctypes.c_size_t,
+                                                   ctypes.c_size_t, c_u64, c_u8p]),
+    "s3dg_last_error": (ctypes.c_char_p, []),
+    "s3dg_version": (ctypes.c_char_p, []),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _f = getattr(_L, _name)   # AttributeError here = the .so does not export the ABI
+    _f.restype, _f.argtypes = _res, _args
+
+lib = _L
+
+
+class S3dgError(RuntimeError):
+    """A failed C-ABI call (negative status); message from s3dg_last_error()."""
+
+    def __init__(self, fn: str, code: int):
+        msg = (_L.s3dg_last_error() or b"").decode(errors="replace")
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+def check(fn: str, code: int) -> None:
+    if code != 0:
+        if code == -1:
+            raise ValueError((_L.s3dg_last_error() or b"").decode(errors="replace"))
+        raise S3dgError(fn, code)
+
+
+def call(fn: str, *args) -> None:
+    check(fn, getattr(_L, fn)(*args))

@@ -1,0 +1,45 @@
+"""Build the C-ABI shared library libs3dlio_amd.so in-tree (gfx950 only).
+
+    python -m s3dlio_amd.build          # or __graft_entry__.build()
+
+Plain hipcc, no CMake: two translation units (kernels + C ABI) linked into
+one .so that exports exactly the symbols of include/s3dlio_gpu.h.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libs3dlio_amd.so")
+SOURCES = [os.path.join(CSRC, "s3dg_kernels.hip"), os.path.join(CSRC, "s3dg_capi.cpp")]
+HEADERS = [os.path.join(CSRC, "s3dg_internal.h"), os.path.join(ROOT, "include", "s3dlio_gpu.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+           "-DS3DG_BUILD", "-o", LIB] + SOURCES
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,475 @@
+// s3dg_capi.cpp — C ABI (include/s3dlio_gpu.h) over the gfx950 kernels.
+//
+// Host-side parameter math follows /root/reference/src/data_gen.rs:151-224:
+// unique_blocks (:162-167), (f_num, f_den) (:169-173), floor_len/rem
+// (:174-175).  No CPU generation path exists in this library: every byte is
+// produced by a HIP kernel, and a missing/failed GPU is an error.
+#include "s3dg_internal.h"
+#include "s3dlio_gpu.h"
+
+#include <sys/random.h>
+#include <time.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+using namespace s3dg;
+
+struct s3dg_ctx {
+    int device = 0;
+    int cus = 256;
+    int wg_per_cu = 4;
+    bool nontemporal = true;
+    void *base_dev = nullptr;          // 4 KiB base block in HBM
+    uint8_t base_host[kBlk];
+    // batch descriptor table (device) + pinned staging, grown on demand
+    ObjEntry *tab_dev = nullptr;
+    ObjEntry *tab_host = nullptr;
+    uint64_t tab_cap = 0;
+    hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
+    std::mutex mu;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hipfail(hipError_t e, const char *what) {
+    return fail(S3DG_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                          \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return hipfail(e_, what); \
+    } while (0)
+
+// SmallRng seeding + Xoshiro256++ on the host, only to derive a base block
+// from a seed (4 KiB, once per set call).
+uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+void base_from_seed(uint64_t seed, uint8_t *out) {
+    uint64_t x = seed, s[4];
+    for (int k = 0; k < 4; ++k) {
+        x += 0x9E3779B97F4A7C15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        s[k] = z ^ (z >> 31);
+    }
+    for (uint32_t off = 0; off < kBlk; off += 8) {
+        const uint64_t r = rotl(s[0] + s[3], 23) + s[0];
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        std::memcpy(out + off, &r, 8);   // little-endian host
+    }
+}
+
+constexpr uint64_t kDefaultBaseSeed = 0xBA5EB10C00000000ull;
+
+int check_ctx(s3dg_ctx *c) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    return S3DG_OK;
+}
+
+int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                PrefixParams *pp) {
+    if (f_den == 0) return fail(S3DG_EINVAL, "f_den must be >= 1");
+    if (f_num >= f_den) return fail(S3DG_EINVAL, "f_num must be < f_den (zero ratio < 1)");
+    if (nblocks > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    const uint64_t tot = (uint64_t)f_num * kBlk;
+    pp->unique = (uint32_t)s3dg_unique_blocks(nblocks, dedup);
+    pp->floor_len = (uint32_t)(tot / f_den);
+    pp->rem = (uint32_t)(tot % f_den);
+    pp->f_den = f_den;
+    return S3DG_OK;
+}
+
+LaunchCfg cfg_for(s3dg_ctx *c, uint64_t tiles) {
+    LaunchCfg lc;
+    uint64_t g = (uint64_t)c->cus * (uint64_t)c->wg_per_cu;
+    const uint64_t need = (tiles + kWavesPerWG - 1) / kWavesPerWG;
+    if (need < g) g = need;
+    lc.grid = (int)(g ? g : 1);
+    lc.nontemporal = c->nontemporal;
+    return lc;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+const char *s3dg_last_error(void) { return g_err.c_str(); }
+const char *s3dg_version(void) { return "s3dlio_amd 0.1.0 (gfx950)"; }
+
+uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup) {
+    const uint64_t d = dedup == 0 ? 1 : dedup;
+    if (d <= 1) return nblocks;
+    double r = std::round((double)nblocks / (double)d);   // f64::round, half away
+    if (r < 1.0) r = 1.0;
+    return (uint64_t)r;
+}
+
+int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den) {
+    if (!f_num || !f_den) return fail(S3DG_EINVAL, "null output");
+    if (compress > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "compress must fit in 32 bits");
+    if (compress > 1) { *f_num = (uint32_t)(compress - 1); *f_den = (uint32_t)compress; }
+    else { *f_num = 0; *f_den = 1; }
+    return S3DG_OK;
+}
+
+uint64_t s3dg_object_entropy(uint64_t seed_base, uint64_t j) { return seed_base + (j << 32); }
+
+int s3dg_device_count(int *out) {
+    if (!out) return fail(S3DG_EINVAL, "null output");
+    HIP_TRY(hipGetDeviceCount(out), "hipGetDeviceCount");
+    return S3DG_OK;
+}
+
+int s3dg_ctx_create(int device, s3dg_ctx **out) {
+    if (!out) return fail(S3DG_EINVAL, "null output");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    if (device < 0 || device >= n) return fail(S3DG_EINVAL, "device index out of range");
+    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    s3dg_ctx *c = new s3dg_ctx();
+    c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+        c->cus = cus;
+    hipError_t e = hipMalloc(&c->base_dev, kBlk);
+    if (e != hipSuccess) { delete c; return hipfail(e, "hipMalloc(base block)"); }
+    e = hipEventCreateWithFlags(&c->tab_free, hipEventDisableTiming);
+    if (e != hipSuccess) { (void)hipFree(c->base_dev); delete c; return hipfail(e, "hipEventCreate"); }
+    base_from_seed(kDefaultBaseSeed, c->base_host);
+    e = hipMemcpy(c->base_dev, c->base_host, kBlk, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { s3dg_ctx_destroy(c); return hipfail(e, "hipMemcpy(base block)"); }
+    *out = c;
+    return S3DG_OK;
+}
+
+int s3dg_ctx_destroy(s3dg_ctx *c) {
+    if (!c) return S3DG_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->base_dev) (void)hipFree(c->base_dev);
+    if (c->tab_dev) (void)hipFree(c->tab_dev);
+    if (c->tab_host) (void)hipHostFree(c->tab_host);
+    if (c->tab_free) (void)hipEventDestroy(c->tab_free);
+    delete c;
+    return S3DG_OK;
+}
+
+int s3dg_set_base_block(s3dg_ctx *c, const uint8_t *base) {
+    if (int r = check_ctx(c)) return r;
+    if (!base) return fail(S3DG_EINVAL, "null base block");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");   // no launch may read the old block
+    std::memcpy(c->base_host, base, kBlk);
+    HIP_TRY(hipMemcpy(c->base_dev, c->base_host, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base)");
+    return S3DG_OK;
+}
+
+int s3dg_set_base_block_seed(s3dg_ctx *c, uint64_t seed) {
+    uint8_t b[kBlk];
+    base_from_seed(seed, b);
+    return s3dg_set_base_block(c, b);
+}
+
+int s3dg_get_base_block(s3dg_ctx *c, uint8_t *out) {
+    if (!c || !out) return fail(S3DG_EINVAL, "null argument");
+    std::memcpy(out, c->base_host, kBlk);
+    return S3DG_OK;
+}
+
+int s3dg_set_occupancy(s3dg_ctx *c, int wg_per_cu) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (wg_per_cu < 0 || wg_per_cu > 8) return fail(S3DG_EINVAL, "wg_per_cu must be 0..8");
+    c->wg_per_cu = wg_per_cu ? wg_per_cu : 4;
+    return S3DG_OK;
+}
+
+int s3dg_set_nontemporal(s3dg_ctx *c, int on) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    c->nontemporal = on != 0;
+    return S3DG_OK;
+}
+
+int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t blk_lo,
+                               uint64_t blk_hi, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                               uint64_t entropy, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (len == 0) return S3DG_OK;                                   // :154-156
+    const uint64_t nb = (len + kBlk - 1) / kBlk;
+    if (blk_hi > nb) blk_hi = nb;
+    if (blk_lo >= blk_hi) return S3DG_OK;
+    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    PrefixParams pp;
+    if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
+    const uint64_t tiles = (blk_hi - blk_lo + kTileBlocks - 1) / kTileBlocks;
+    HIP_TRY(launch_fill_stream(cfg_for(c, tiles), (uint8_t *)dst, len, 0, 1, (uint32_t)blk_lo,
+                               (uint32_t)blk_hi, entropy, 0, pp, c->base_dev,
+                               (hipStream_t)stream),
+            "launch k_fill_stream");
+    return S3DG_OK;
+}
+
+int s3dg_fill_controlled(s3dg_ctx *c, void *dst, uint64_t len, uint64_t dedup, uint32_t f_num,
+                         uint32_t f_den, uint64_t entropy, void *stream) {
+    return s3dg_fill_controlled_range(c, dst, len, 0, ~0ull, dedup, f_num, f_den, entropy, stream);
+}
+
+int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride,
+                                uint64_t n_objs, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                                uint64_t seed_base, uint64_t first_obj, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (obj_size == 0 || n_objs == 0) return S3DG_OK;
+    if (!dst || !aligned16(dst) || (stride & 15u))
+        return fail(S3DG_EINVAL, "dst and stride must be 16-byte aligned");
+    if (n_objs > 1 && stride < obj_size) return fail(S3DG_EINVAL, "stride < obj_size: objects overlap");
+    const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
+    PrefixParams pp;
+    if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
+    const uint64_t tiles = (nb + kTileBlocks - 1) / kTileBlocks * n_objs;
+    HIP_TRY(launch_fill_stream(cfg_for(c, tiles), (uint8_t *)dst, obj_size, stride, n_objs, 0,
+                               (uint32_t)nb, seed_base, first_obj, pp, c->base_dev,
+                               (hipStream_t)stream),
+            "launch k_fill_stream");
+    return S3DG_OK;
+}
+
+int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc *d, uint64_t n,
+                               void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (n == 0) return S3DG_OK;
+    if (!d) return fail(S3DG_EINVAL, "null descriptor array");
+    if (!dst_base || !aligned16(dst_base)) return fail(S3DG_EINVAL, "dst_base must be 16-byte aligned");
+    std::lock_guard<std::mutex> g(c->mu);
+    // the previous batch's upload must have left the pinned staging table
+    HIP_TRY(hipEventSynchronize(c->tab_free), "hipEventSynchronize");
+    if (n > c->tab_cap) {
+        if (c->tab_dev) (void)hipFree(c->tab_dev);
+        if (c->tab_host) (void)hipHostFree(c->tab_host);
+        c->tab_dev = nullptr; c->tab_host = nullptr; c->tab_cap = 0;
+        uint64_t cap = n < 1024 ? 1024 : n;
+        HIP_TRY(hipMalloc(&c->tab_dev, cap * sizeof(ObjEntry)), "hipMalloc(batch table)");
+        HIP_TRY(hipHostMalloc(&c->tab_host, cap * sizeof(ObjEntry), hipHostMallocDefault),
+                "hipHostMalloc(batch table)");
+        c->tab_cap = cap;
+    }
+    // Objects of size 0 contribute no tiles; the search skips them because
+    // the next entry has the same tile_begin.
+    uint64_t tiles = 0, m = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+        if (d[k].size == 0) continue;
+        if (d[k].dst_off & 15u) return fail(S3DG_EINVAL, "dst_off must be a multiple of 16");
+        const uint64_t nb = (d[k].size + kBlk - 1) / kBlk;
+        ObjEntry &e = c->tab_host[m++];
+        e.dst_off = d[k].dst_off;
+        e.size = d[k].size;
+        e.entropy = d[k].entropy;
+        e.tile_begin = tiles;
+        if (int r = make_prefix(nb, d[k].dedup, d[k].f_num, d[k].f_den, &e.pp)) return r;
+        tiles += (nb + kTileBlocks - 1) / kTileBlocks;
+    }
+    if (m == 0) return S3DG_OK;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(c->tab_dev, c->tab_host, m * sizeof(ObjEntry), hipMemcpyHostToDevice, s),
+            "hipMemcpyAsync(batch table)");
+    HIP_TRY(hipEventRecord(c->tab_free, s), "hipEventRecord");
+    HIP_TRY(launch_fill_batch(cfg_for(c, tiles), (uint8_t *)dst_base, c->tab_dev, m, tiles,
+                              c->base_dev, s),
+            "launch k_fill_batch");
+    return S3DG_OK;
+}
+
+int s3dg_write_ceiling(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (!dst || !aligned16(dst) || (len & 15u)) return fail(S3DG_EINVAL, "dst/len must be 16-byte aligned");
+    LaunchCfg lc = cfg_for(c, ~0ull >> 8);
+    HIP_TRY(launch_write_ceiling(lc, (uint8_t *)dst, len, pattern, (hipStream_t)stream),
+            "launch k_write_ceiling");
+    return S3DG_OK;
+}
+
+int s3dg_device_alloc(s3dg_ctx *c, uint64_t bytes, void **out) {
+    if (int r = check_ctx(c)) return r;
+    if (!out) return fail(S3DG_EINVAL, "null output");
+    HIP_TRY(hipMalloc(out, bytes), "hipMalloc");
+    return S3DG_OK;
+}
+
+int s3dg_device_free(s3dg_ctx *c, void *p) {
+    if (int r = check_ctx(c)) return r;
+    HIP_TRY(hipFree(p), "hipFree");
+    return S3DG_OK;
+}
+
+int s3dg_host_alloc_pinned(uint64_t bytes, void **out) {
+    if (!out) return fail(S3DG_EINVAL, "null output");
+    HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocDefault), "hipHostMalloc");
+    return S3DG_OK;
+}
+
+int s3dg_host_free_pinned(void *p) {
+    HIP_TRY(hipHostFree(p), "hipHostFree");
+    return S3DG_OK;
+}
+
+int s3dg_d2h_async(s3dg_ctx *c, void *host, const void *dev, uint64_t len, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    HIP_TRY(hipMemcpyAsync(host, dev, len, hipMemcpyDeviceToHost, (hipStream_t)stream),
+            "hipMemcpyAsync(D2H)");
+    return S3DG_OK;
+}
+
+int s3dg_h2d_async(s3dg_ctx *c, void *dev, const void *host, uint64_t len, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    HIP_TRY(hipMemcpyAsync(dev, host, len, hipMemcpyHostToDevice, (hipStream_t)stream),
+            "hipMemcpyAsync(H2D)");
+    return S3DG_OK;
+}
+
+int s3dg_stream_create(s3dg_ctx *c, void **out) {
+    if (int r = check_ctx(c)) return r;
+    if (!out) return fail(S3DG_EINVAL, "null output");
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    *out = (void *)s;
+    return S3DG_OK;
+}
+
+int s3dg_stream_destroy(s3dg_ctx *c, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+    return S3DG_OK;
+}
+
+int s3dg_sync(s3dg_ctx *c, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+    else HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    return S3DG_OK;
+}
+
+}  // extern "C"
+
+// ---- host-buffer drop-ins ----------------------------------------------------
+
+namespace {
+
+struct DefaultCtx {
+    std::mutex mu;
+    s3dg_ctx *ctx = nullptr;
+    uint8_t proc_base[kBlk];           // A_BASE_BLOCK equivalent (random, once per process)
+    bool have_proc_base = false;
+    void *scratch[2] = {nullptr, nullptr};
+    hipStream_t st[2] = {nullptr, nullptr};
+    static constexpr uint64_t kChunk = 64ull << 20;   // 64 MiB per device chunk
+};
+
+DefaultCtx &dflt() {
+    static DefaultCtx *d = new DefaultCtx();   // intentionally leaked: outlives atexit
+    return *d;
+}
+
+int dflt_init(DefaultCtx &D) {
+    if (D.ctx) return S3DG_OK;
+    int dev = 0;
+    if (const char *e = getenv("S3DLIO_GPU_DEVICE")) dev = atoi(e);
+    if (int r = s3dg_ctx_create(dev, &D.ctx)) return r;
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(hipMalloc(&D.scratch[k], DefaultCtx::kChunk), "hipMalloc(scratch)");
+        HIP_TRY(hipStreamCreateWithFlags(&D.st[k], hipStreamNonBlocking), "hipStreamCreate");
+    }
+    return S3DG_OK;
+}
+
+// Generate into a host buffer through two 64 MiB device chunks on two
+// streams, so chunk k+1's kernel overlaps chunk k's D2H copy.
+int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t dedup, uint64_t compress,
+              uint64_t entropy) {
+    uint32_t fn, fd;
+    if (int r = s3dg_compress_ratio(compress, &fn, &fd)) return r;
+    const uint64_t nb = (len + kBlk - 1) / kBlk;
+    const uint64_t cb = DefaultCtx::kChunk / kBlk;
+    for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
+        const uint64_t b1 = b0 + cb < nb ? b0 + cb : nb;
+        const int sl = (int)(k & 1);
+        if (int r = s3dg_fill_controlled_range(D.ctx, D.scratch[sl], len, b0, b1, dedup, fn, fd,
+                                               entropy, D.st[sl]))
+            return r;
+        const uint64_t off = b0 * kBlk;
+        const uint64_t n = (b1 * kBlk < len ? b1 * kBlk : len) - off;
+        HIP_TRY(hipMemcpyAsync(buf + off, D.scratch[sl], n, hipMemcpyDeviceToHost, D.st[sl]),
+                "hipMemcpyAsync(D2H)");
+    }
+    HIP_TRY(hipStreamSynchronize(D.st[0]), "hipStreamSynchronize");
+    HIP_TRY(hipStreamSynchronize(D.st[1]), "hipStreamSynchronize");
+    return S3DG_OK;
+}
+
+uint64_t time_entropy() {      // SystemTime::now() ... as_nanos() as u64, :192-195
+    timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+}  // namespace
+
+extern "C" {
+
+int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress) {
+    if (len == 0) return S3DG_OK;
+    if (!buf) return fail(S3DG_EINVAL, "null buffer");
+    DefaultCtx &D = dflt();
+    std::lock_guard<std::mutex> g(D.mu);
+    if (int r = dflt_init(D)) return r;
+    if (!D.have_proc_base) {
+        size_t got = 0;
+        while (got < kBlk) {
+            ssize_t k = getrandom(D.proc_base + got, kBlk - got, 0);
+            if (k <= 0) return fail(S3DG_EINVAL, "getrandom failed");
+            got += (size_t)k;
+        }
+        D.have_proc_base = true;
+    }
+    uint8_t saved[kBlk];
+    std::memcpy(saved, D.ctx->base_host, kBlk);
+    if (int r = s3dg_set_base_block(D.ctx, D.proc_base)) return r;
+    int r = fill_host(D, buf, len, dedup, compress, time_entropy());
+    int r2 = s3dg_set_base_block(D.ctx, saved);
+    return r ? r : r2;
+}
+
+int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, size_t compress,
+                                       uint64_t entropy, const uint8_t *base4096) {
+    if (len == 0) return S3DG_OK;
+    if (!buf) return fail(S3DG_EINVAL, "null buffer");
+    DefaultCtx &D = dflt();
+    std::lock_guard<std::mutex> g(D.mu);
+    if (int r = dflt_init(D)) return r;
+    if (!base4096) return fill_host(D, buf, len, dedup, compress, entropy);
+    uint8_t saved[kBlk];
+    std::memcpy(saved, D.ctx->base_host, kBlk);
+    if (int r = s3dg_set_base_block(D.ctx, base4096)) return r;
+    int r = fill_host(D, buf, len, dedup, compress, entropy);
+    int r2 = s3dg_set_base_block(D.ctx, saved);
+    return r ? r : r2;
+}
+
+}  // extern "C"

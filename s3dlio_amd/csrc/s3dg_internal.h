@@ -1,0 +1,50 @@
+// s3dg_internal.h — shared between the HIP kernels and the C-ABI layer.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace s3dg {
+
+constexpr uint32_t kBlk = 4096;   // BLK_SIZE   src/constants.rs:326
+constexpr uint32_t kHalf = 2048;  // HALF_BLK   src/constants.rs:329
+constexpr uint32_t kMod = 32;     // MOD_SIZE   src/constants.rs:352
+constexpr uint32_t kTileBlocks = 64;  // blocks per wave tile (one per lane)
+constexpr int kWavesPerWG = 4;
+
+// Zero-prefix parameters of one object: const_len(u) =
+//   floor_len + ((u+1)*rem)/f_den - (u*rem)/f_den   (closed form of the
+// accumulator at src/data_gen.rs:174-190; rem < f_den).
+struct PrefixParams {
+    uint32_t unique;     // U, src/data_gen.rs:162-167
+    uint32_t floor_len;
+    uint32_t rem;
+    uint32_t f_den;
+};
+
+// Device-side table entry of a mixed-size batch (48 B).
+struct ObjEntry {
+    uint64_t dst_off;
+    uint64_t size;
+    uint64_t entropy;
+    uint64_t tile_begin;   // exclusive prefix sum of ceil(nblocks/64)
+    PrefixParams pp;
+};
+
+struct LaunchCfg {
+    int grid;        // workgroups (persistent, grid-stride over tiles)
+    bool nontemporal;
+};
+
+hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size,
+                              uint64_t stride, uint64_t n_objs, uint32_t blk_lo,
+                              uint32_t blk_hi, uint64_t seed_base, uint64_t first_obj,
+                              PrefixParams pp, const void *base_dev, hipStream_t s);
+
+hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
+                             uint64_t n, uint64_t total_tiles, const void *base_dev,
+                             hipStream_t s);
+
+hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
+                                uint32_t pattern, hipStream_t s);
+
+}  // namespace s3dg

@@ -1,0 +1,232 @@
+"""GPU parity: the gfx950 kernels through the C ABI vs the golden fixtures and
+the C oracle (bit-exact; integer/byte work, no tolerance)."""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import oracle_py as P
+
+pytestmark = pytest.mark.gpu
+
+SEED_BASE = 0x5EED000000000001
+GUARD = 0xAB
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    return torch
+
+
+@pytest.fixture(scope="module")
+def base(golden_base):
+    return np.frombuffer(golden_base, np.uint8)
+
+
+def test_base_block_matches_fixture(gpu_ctx, golden_base):
+    assert gpu_ctx.base_block == golden_base
+
+
+def test_cfg1_golden_digests(gpu_ctx, torch):
+    g = load("cfg1_1000x64KiB.json")
+    n, size = g["objects"], g["size"]
+    out = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_stream(out, obj_size=size, n_objs=n, seed_base=int(g["seed_base"], 16))
+    torch.cuda.synchronize()
+    host = out.cpu().numpy()
+    digests = [sha(host[j * size:(j + 1) * size]) for j in range(n)]
+    assert digests == g["sha256"]
+
+
+def test_edge_case_fixtures_with_guards(gpu_ctx, torch):
+    cases = load("edge_cases.json")["cases"]
+    maxlen = max(c["len"] for c in cases)
+    buf = torch.empty(maxlen + 256, dtype=torch.uint8, device="cuda")
+    bad = []
+    for c in cases:
+        buf.fill_(GUARD)
+        gpu_ctx.fill_controlled(buf, c["len"], dedup=c["dedup"],
+                                compress=(c["f_den"], c["f_den"] - c["f_num"]) if c["f_num"] else 1,
+                                entropy=int(c["entropy"]))
+        h = buf[:c["len"] + 256].cpu().numpy()
+        if sha(h[:c["len"]]) != c["sha256"] or not (h[c["len"]:] == GUARD).all():
+            bad.append(c)
+    assert not bad, bad[:3]
+
+
+def test_blob_fixtures(gpu_ctx, torch):
+    for name, (L, d, comp, e) in {"blob_4097_d1_c3": (4097, 1, 3, 11),
+                                  "blob_12288_d2_c2": (12288, 2, 2, 12),
+                                  "blob_8192_d1_c1": (8192, 1, 1, 13)}.items():
+        with open(os.path.join(GOLDEN, name + ".bin"), "rb") as f:
+            exp = f.read()
+        t = torch.empty(L, dtype=torch.uint8, device="cuda")
+        gpu_ctx.fill_controlled(t, L, dedup=d, compress=comp, entropy=e)
+        assert bytes(t.cpu().numpy()) == exp, name
+
+
+@pytest.mark.parametrize("size,stride,n,d,c,first", [
+    (8 * 2**20, 8 * 2**20, 24, 1, 1, 0),
+    (8 * 2**20, 8 * 2**20, 24, 4, 2, 7),
+    (8 * 2**20, 8 * 2**20, 24, 2, 3, 123456),
+    (4096 * 70 + 1000, 4096 * 72, 9, 3, 5, 3),
+    (4096 * 64, 4096 * 64, 5, 1, 2, 0),
+    (1, 16, 33, 1, 1, 0),
+    (4095, 4096, 17, 2, 129, 2**20),
+])
+def test_stream_vs_oracle(gpu_ctx, torch, oracle, base, size, stride, n, d, c, first):
+    fn, fd = P.compress_ratio(c)
+    out = torch.full((stride * n + 64,), GUARD, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_stream(out, obj_size=size, n_objs=n, stride=stride, dedup=d, compress=c,
+                        seed_base=SEED_BASE, first_obj=first)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    exp = oracle.fill_stream(size, n, d, fn, fd, SEED_BASE, first, base, stride=stride, threads=8)
+    for j in range(n):
+        o = j * stride
+        assert np.array_equal(got[o:o + size], exp[o:o + size]), j
+        assert (got[o + size:o + stride] == GUARD).all(), f"gap overwritten after object {j}"
+    assert (got[stride * n:] == GUARD).all()
+
+
+def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base):
+    rnd = random.Random(7)
+    sizes = [0, 1, 5, 31, 32, 33, 4095, 4096, 4097, 2**20 + 3, 3 * 2**20, 65536 * 64 + 11]
+    sizes += [int(np.exp(rnd.uniform(np.log(4096), np.log(4 * 2**20)))) for _ in range(40)]
+    objs, off = [], 0
+    for j, sz in enumerate(sizes):
+        d = rnd.choice([0, 1, 2, 3, 4, 100])
+        c = rnd.choice([1, 2, 3, 7, (3, 2), (5, 3)])
+        objs.append((off, sz, P.object_entropy(SEED_BASE, j), d, c))
+        off += (sz + 16 + 4095) // 4096 * 4096          # a guard gap after each object
+    out = torch.full((off,), GUARD, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_batch(out, objs)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    nxt = [o[0] for o in objs[1:]] + [off]
+    for (o, sz, e, d, c), end in zip(objs, nxt):
+        fn, fd = P.compress_ratio(c)
+        exp = oracle.fill_controlled(sz, d, fn, fd, e, base)
+        assert np.array_equal(got[o:o + sz], exp), (o, sz, d, c)
+        assert (got[o + sz:end] == GUARD).all()
+
+
+def test_range_pieces_compose(gpu_ctx, torch, oracle, base):
+    L = 4096 * 300 + 77
+    full = torch.empty(L, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_controlled(full, L, dedup=3, compress=3, entropy=31337)
+    pieces = torch.empty(L, dtype=torch.uint8, device="cuda")
+    for lo, hi in [(0, 1), (1, 65), (65, 130), (130, 301)]:
+        view = pieces[lo * 4096:]
+        gpu_ctx.fill_range(view, L, lo, hi, dedup=3, compress=3, entropy=31337)
+    torch.cuda.synchronize()
+    assert torch.equal(full, pieces)
+    assert bytes(full.cpu().numpy()) == bytes(oracle.fill_controlled(L, 3, 2, 3, 31337, base))
+
+
+def test_store_modes_and_occupancy_agree(gpu_ctx, torch):
+    n, size = 40, 2**20 + 4096 * 3
+    ref = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_stream(ref, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
+    for nt in (False, True):
+        for occ in (1, 2, 8):
+            gpu_ctx.set_nontemporal(nt)
+            gpu_ctx.set_occupancy(occ)
+            t = torch.zeros_like(ref)
+            gpu_ctx.fill_stream(t, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
+            assert torch.equal(t, ref), (nt, occ)
+    gpu_ctx.set_nontemporal(True)
+    gpu_ctx.set_occupancy(0)
+
+
+def test_host_dropin_seeded_multi_chunk(oracle, base):
+    import s3dlio_amd as S
+    L = 150 * 2**20 + 5                      # > two 64 MiB device chunks, ragged tail
+    buf = bytearray(L)
+    S.fill_controlled_data_seeded(buf, 2, 3, entropy=77, base_block=bytes(base))
+    exp = oracle.fill_controlled(L, 2, 2, 3, 77, base)
+    assert sha(buf) == sha(exp)
+    arr = np.zeros(12345, np.uint8)
+    S.fill_controlled_data_seeded(arr, 1, 1, entropy=9)          # default base block
+    assert np.array_equal(arr, oracle.fill_controlled(12345, 1, 0, 1, 9, base))
+
+
+def test_host_dropin_unseeded_contract():
+    """Reference unit tests (src/data_gen.rs:405-458): size preserved, not all
+    zero, two calls differ, empty buffer ok, dedup/compress accepted."""
+    import s3dlio_amd as S
+    a, b = bytearray(2**20), bytearray(2**20)
+    S.fill_controlled_data(a, 1, 1)
+    S.fill_controlled_data(b, 1, 1)
+    assert len(a) == 2**20 and any(a) and a != b
+    S.fill_controlled_data(bytearray(), 1, 1)
+    c = bytearray(4 * 2**20)
+    S.fill_controlled_data(c, 4, 1)
+    blocks = {bytes(c[i:i + 4096]) for i in range(0, len(c), 4096)}
+    assert len(blocks) == 256
+    z = bytearray(2 * 2**20)
+    S.fill_controlled_data(z, 1, 4)
+    assert abs(z.count(0) / len(z) - 0.75) < 0.01
+
+
+def test_full_size_structure_cfg2(gpu_ctx, torch, base):
+    """Size-independent properties at BASELINE cfg2 object size on 1000 x 8 MiB
+    (7.8 GiB): every block equals the base block outside the two 32-byte
+    windows [0,32) and [2048,2080); windows differ between blocks."""
+    n, size = 1000, 8 * 2**20
+    out = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_stream(out, obj_size=size, n_objs=n, seed_base=SEED_BASE)
+    blocks = out.view(-1, 4096)
+    bt = torch.from_numpy(base.copy()).cuda()
+    mask = torch.ones(4096, dtype=torch.bool, device="cuda")
+    mask[0:32] = False
+    mask[2048:2080] = False
+    assert torch.equal(blocks[:, mask], bt[mask].expand(blocks.shape[0], -1))
+    w = blocks[:, 0:8].contiguous().view(torch.int64).flatten()
+    assert torch.unique(w).numel() == w.numel()          # 2,048,000 distinct first words
+    del out, blocks
+
+
+def test_full_size_structure_cfg3(gpu_ctx, torch, oracle, base):
+    """cfg3 (dedup=4, compress=2) at 8 MiB: U=512 unique blocks repeating with
+    period 512, zero prefix exactly 2048 B, sampled objects bit-exact."""
+    n, size = 200, 8 * 2**20
+    out = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_stream(out, obj_size=size, n_objs=n, dedup=4, compress=2, seed_base=SEED_BASE)
+    v = out.view(n, 4, 512, 4096)
+    for r in range(1, 4):
+        assert torch.equal(v[:, 0], v[:, r])
+    assert int(v[..., :2048].count_nonzero()) == 0
+    for j in (0, 57, n - 1):
+        exp = oracle.fill_controlled(size, 4, 1, 2, P.object_entropy(SEED_BASE, j), base)
+        assert bytes(out[j * size:(j + 1) * size].cpu().numpy()) == bytes(exp)
+
+
+def test_write_ceiling_kernel(gpu_ctx, torch):
+    t = torch.zeros(2**24, dtype=torch.uint8, device="cuda")
+    gpu_ctx.write_ceiling(t, pattern=0x01020304)
+    torch.cuda.synchronize()
+    w = t.view(torch.int32).view(-1, 4)
+    assert int(w[:, 0].eq(0x01020304).all()) == 1
+
+
+def test_invalid_arguments_raise(gpu_ctx, torch):
+    t = torch.empty(4096 + 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError, match="aligned"):
+        gpu_ctx.fill_controlled(int(t.data_ptr()) + 1, 100)
+    with pytest.raises(ValueError):
+        gpu_ctx.fill_stream(t, obj_size=4096, n_objs=2, stride=100)
