@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--ring-gib", type=float, default=80.0,
                    help="device output ring per GPU (objects wrap when the step exceeds it)")
     p.add_argument("--occupancy", type=int, default=None, help="workgroups per CU")
-    p.add_argument("--plain-stores", action="store_true", help="disable nontemporal stores")
+    p.add_argument("--nt-stores", action="store_true", help="nontemporal stores (default plain)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")
@@ -97,7 +97,7 @@ def main() -> int:
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
     ctx = Context(dev, base_seed=BASE_SEED, occupancy=args.occupancy,
-                  nontemporal=not args.plain_stores)
+                  nontemporal=args.nt_stores)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     fn, fd = compress_ratio(cfg["compress"])
@@ -208,7 +208,7 @@ def main() -> int:
         verified = bool(cp.max(0.0 if ok else 1.0) == 0.0)
 
     # ---- write-only ceiling on the same buffer (same store path) -----------------------
-    ceil_bytes = min(int(ring.numel()), 16 * GiB) // 16 * 16
+    ceil_bytes = min(int(ring.numel()), 16 * GiB) // 4096 * 4096
     ctx.write_ceiling(ring, ceil_bytes, stream=stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -246,11 +246,12 @@ def main() -> int:
                        "bytes_per_step_all_ranks": int(total_bytes // args.steps),
                        "dedup": cfg["dedup"], "compress": list(cfg["compress"]) if isinstance(cfg["compress"], tuple) else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
-                       "stores": "plain" if args.plain_stores else "nontemporal"},
+                       "stores": "nontemporal" if args.nt_stores else "plain"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic_from_profiles(),
                          "kernel": "k_fill_stream" if cfg["size"] else "k_fill_batch",
+                         "launch_shape": "one 256-thread workgroup per 4 KiB block",
                          "avg_launch_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": int(sum(launch_bytes) / len(launch_bytes)),
                          "write_ceiling_GBps": round(ceiling_gbs, 1),

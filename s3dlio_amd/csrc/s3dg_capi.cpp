@@ -21,15 +21,15 @@ using namespace s3dg;
 
 struct s3dg_ctx {
     int device = 0;
-    int cus = 256;
-    int wg_per_cu = 4;
-    bool nontemporal = true;
+    bool nontemporal = false;          // plain stores measured faster
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // batch descriptor table (device) + pinned staging, grown on demand
     ObjEntry *tab_dev = nullptr;
     ObjEntry *tab_host = nullptr;
     uint64_t tab_cap = 0;
+    uint32_t *tile_obj = nullptr;      // tile -> object entry map (device)
+    uint64_t tile_cap = 0;
     hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
     std::mutex mu;
 };
@@ -88,19 +88,18 @@ int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den
     if (f_num >= f_den) return fail(S3DG_EINVAL, "f_num must be < f_den (zero ratio < 1)");
     if (nblocks > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
     const uint64_t tot = (uint64_t)f_num * kBlk;
-    pp->unique = (uint32_t)s3dg_unique_blocks(nblocks, dedup);
+    const uint64_t U = s3dg_unique_blocks(nblocks, dedup);
+    pp->unique = U == nblocks ? 0xFFFFFFFFu : (uint32_t)U;
     pp->floor_len = (uint32_t)(tot / f_den);
     pp->rem = (uint32_t)(tot % f_den);
     pp->f_den = f_den;
+    pp->m_unique = fastmod_magic(pp->unique == 0xFFFFFFFFu ? 1u : pp->unique);
+    pp->m_fden = fastmod_magic(f_den);
     return S3DG_OK;
 }
 
-LaunchCfg cfg_for(s3dg_ctx *c, uint64_t tiles) {
+LaunchCfg cfg_for(s3dg_ctx *c) {
     LaunchCfg lc;
-    uint64_t g = (uint64_t)c->cus * (uint64_t)c->wg_per_cu;
-    const uint64_t need = (tiles + kWavesPerWG - 1) / kWavesPerWG;
-    if (need < g) g = need;
-    lc.grid = (int)(g ? g : 1);
     lc.nontemporal = c->nontemporal;
     return lc;
 }
@@ -147,10 +146,6 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
     HIP_TRY(hipSetDevice(device), "hipSetDevice");
     s3dg_ctx *c = new s3dg_ctx();
     c->device = device;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
-        cus > 0)
-        c->cus = cus;
     hipError_t e = hipMalloc(&c->base_dev, kBlk);
     if (e != hipSuccess) { delete c; return hipfail(e, "hipMalloc(base block)"); }
     e = hipEventCreateWithFlags(&c->tab_free, hipEventDisableTiming);
@@ -169,6 +164,7 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     if (c->base_dev) (void)hipFree(c->base_dev);
     if (c->tab_dev) (void)hipFree(c->tab_dev);
     if (c->tab_host) (void)hipHostFree(c->tab_host);
+    if (c->tile_obj) (void)hipFree(c->tile_obj);
     if (c->tab_free) (void)hipEventDestroy(c->tab_free);
     delete c;
     return S3DG_OK;
@@ -197,9 +193,10 @@ int s3dg_get_base_block(s3dg_ctx *c, uint8_t *out) {
 }
 
 int s3dg_set_occupancy(s3dg_ctx *c, int wg_per_cu) {
+    // Kept for ABI stability: the kernels are non-persistent (one workgroup
+    // per 4 KiB block), so residency is left to the hardware dispatcher.
     if (!c) return fail(S3DG_EINVAL, "null context");
     if (wg_per_cu < 0 || wg_per_cu > 8) return fail(S3DG_EINVAL, "wg_per_cu must be 0..8");
-    c->wg_per_cu = wg_per_cu ? wg_per_cu : 4;
     return S3DG_OK;
 }
 
@@ -220,8 +217,7 @@ int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t bl
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
     PrefixParams pp;
     if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
-    const uint64_t tiles = (blk_hi - blk_lo + kTileBlocks - 1) / kTileBlocks;
-    HIP_TRY(launch_fill_stream(cfg_for(c, tiles), (uint8_t *)dst, len, 0, 1, (uint32_t)blk_lo,
+    HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, len, 0, 1, (uint32_t)blk_lo,
                                (uint32_t)blk_hi, entropy, 0, pp, c->base_dev,
                                (hipStream_t)stream),
             "launch k_fill_stream");
@@ -244,8 +240,7 @@ int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint6
     const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
     PrefixParams pp;
     if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
-    const uint64_t tiles = (nb + kTileBlocks - 1) / kTileBlocks * n_objs;
-    HIP_TRY(launch_fill_stream(cfg_for(c, tiles), (uint8_t *)dst, obj_size, stride, n_objs, 0,
+    HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, obj_size, stride, n_objs, 0,
                                (uint32_t)nb, seed_base, first_obj, pp, c->base_dev,
                                (hipStream_t)stream),
             "launch k_fill_stream");
@@ -287,21 +282,31 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         tiles += (nb + kTileBlocks - 1) / kTileBlocks;
     }
     if (m == 0) return S3DG_OK;
+    if (tiles > c->tile_cap) {
+        // the previous batch may still read the old map: it is stream-ordered
+        // only on its own stream, so drain the device before freeing
+        HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        if (c->tile_obj) (void)hipFree(c->tile_obj);
+        c->tile_obj = nullptr; c->tile_cap = 0;
+        const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
+        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(uint32_t)), "hipMalloc(tile map)");
+        c->tile_cap = cap;
+    }
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemcpyAsync(c->tab_dev, c->tab_host, m * sizeof(ObjEntry), hipMemcpyHostToDevice, s),
             "hipMemcpyAsync(batch table)");
     HIP_TRY(hipEventRecord(c->tab_free, s), "hipEventRecord");
-    HIP_TRY(launch_fill_batch(cfg_for(c, tiles), (uint8_t *)dst_base, c->tab_dev, m, tiles,
-                              c->base_dev, s),
+    HIP_TRY(launch_fill_batch(cfg_for(c), (uint8_t *)dst_base, c->tab_dev, m, tiles,
+                              c->tile_obj, c->base_dev, s),
             "launch k_fill_batch");
     return S3DG_OK;
 }
 
 int s3dg_write_ceiling(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, void *stream) {
     if (int r = check_ctx(c)) return r;
-    if (!dst || !aligned16(dst) || (len & 15u)) return fail(S3DG_EINVAL, "dst/len must be 16-byte aligned");
-    LaunchCfg lc = cfg_for(c, ~0ull >> 8);
-    HIP_TRY(launch_write_ceiling(lc, (uint8_t *)dst, len, pattern, (hipStream_t)stream),
+    if (!dst || !aligned16(dst) || (len % kBlk))
+        return fail(S3DG_EINVAL, "dst must be 16-byte aligned and len a multiple of 4096");
+    HIP_TRY(launch_write_ceiling(cfg_for(c), (uint8_t *)dst, len, pattern, (hipStream_t)stream),
             "launch k_write_ceiling");
     return S3DG_OK;
 }

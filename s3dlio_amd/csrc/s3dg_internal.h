@@ -8,20 +8,26 @@ namespace s3dg {
 constexpr uint32_t kBlk = 4096;   // BLK_SIZE   src/constants.rs:326
 constexpr uint32_t kHalf = 2048;  // HALF_BLK   src/constants.rs:329
 constexpr uint32_t kMod = 32;     // MOD_SIZE   src/constants.rs:352
-constexpr uint32_t kTileBlocks = 64;  // blocks per wave tile (one per lane)
+constexpr uint32_t kTileBlocks = 64;  // blocks per batch tile (tile -> object map granule)
 constexpr int kWavesPerWG = 4;
 
 // Zero-prefix parameters of one object: const_len(u) =
 //   floor_len + ((u+1)*rem)/f_den - (u*rem)/f_den   (closed form of the
 // accumulator at src/data_gen.rs:174-190; rem < f_den).
 struct PrefixParams {
-    uint32_t unique;     // U, src/data_gen.rs:162-167
+    uint32_t unique;     // U, src/data_gen.rs:162-167 (0xFFFFFFFF: U == nblocks, u = i)
     uint32_t floor_len;
     uint32_t rem;
     uint32_t f_den;
+    uint64_t m_unique;   // Lemire fastmod constants: floor(2^64 / d) + 1
+    uint64_t m_fden;
 };
 
-// Device-side table entry of a mixed-size batch (48 B).
+// a % d for 32-bit a and d >= 1 with M = fastmod_magic(d) (Lemire, Kaser &
+// Kurz 2019, "Faster remainder by direct computation"); exact for all a, d < 2^32.
+inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
+
+// Device-side table entry of a mixed-size batch (64 B).
 struct ObjEntry {
     uint64_t dst_off;
     uint64_t size;
@@ -31,7 +37,6 @@ struct ObjEntry {
 };
 
 struct LaunchCfg {
-    int grid;        // workgroups (persistent, grid-stride over tiles)
     bool nontemporal;
 };
 
@@ -41,8 +46,8 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               PrefixParams pp, const void *base_dev, hipStream_t s);
 
 hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, const void *base_dev,
-                             hipStream_t s);
+                             uint64_t n, uint64_t total_tiles, uint32_t *tile_obj,
+                             const void *base_dev, hipStream_t s);
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
                                 uint32_t pattern, hipStream_t s);

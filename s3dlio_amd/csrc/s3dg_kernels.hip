@@ -2,31 +2,38 @@
 // generator.  Semantics: /root/reference/src/data_gen.rs:151-224
 // (fill_controlled_data), bit-exact for a given entropy and base block.
 //
-// Work decomposition:
-//   * A "tile" = up to 64 consecutive 4 KiB blocks of ONE object, owned by
-//     one wave64.  Lane l first computes everything block (tile_first + l)
-//     needs — u = i % U, the zero-prefix length, the SplitMix64 seed
-//     expansion and the <= 8 Xoshiro256++ draws of its two 32-byte windows —
-//     so the sequential-PRNG work is spread one block per lane.  The window
-//     bytes go to a per-wave LDS image, the scalar block metadata stays in
-//     VGPRs and is broadcast with v_readlane.
-//   * The wave then writes its 64 blocks in order: 4 x 1 KiB
-//     global_store_dwordx4 per block (16 B per lane, fully coalesced), data =
-//     the base block held in 16 VGPRs per lane, or zeros.  Only the <= 6
-//     lane-segments per block that straddle a window / the zero boundary /
-//     the object tail take the masked slow path (LDS window read +
-//     v_alignbyte).  No HBM reads: dedup blocks are recomputed, not copied.
-//   * Persistent grid (CUs x wg_per_cu workgroups of 4 waves), grid-stride
-//     over tiles.  Write-only streaming: there is no reuse, so the block->XCD
-//     placement only matters for load balance.
+// Work decomposition (measurements in profiles/):
+//   * ONE 256-thread workgroup per 4 KiB block, non-persistent grid in
+//     address order.  Each of the 4 waves writes one 1 KiB quarter with a
+//     single 16-byte store per lane (global_store_dwordx4).  Measured on
+//     MI355X this is the write pattern that reaches the HBM write ceiling
+//     (6.9-7.0 TB/s, = hipMemset-class fill): short-lived workgroups
+//     dispatched in order keep the write frontier compact, whereas
+//     persistent or multi-block workgroups stay at 5.0-6.3 TB/s.
+//   * Wave 0 derives the block's parameters (u = i % U, zero-prefix length,
+//     window offsets) and runs the block's PRNG chain ONCE (SplitMix64 seed
+//     expansion + <= 8 Xoshiro256++ draws; wave-uniform, so it runs on the
+//     scalar unit), publishes them to LDS, then a workgroup barrier.  Running
+//     the chain in more than one wave per block made the kernel
+//     compute-bound (64-bit multiplies), see DESIGN.md.
+//   * Every lane then stores base-block bytes (16 B per lane, read once per
+//     workgroup from L2) or zeros; only the <= 6 lanes per block that straddle
+//     a window / the zero boundary / the object tail take the byte-masked
+//     slow path (LDS window image + v_alignbyte).  No HBM reads: dedup blocks
+//     are recomputed, never copied.
 #include "s3dg_internal.h"
+
+// Diagnostic builds only (tools/ablate.py): bit 0 = no window patch phase,
+// bit 1 = no PRNG chain.  Outputs of such builds are wrong by design.
+#ifndef S3DG_ABLATE
+#define S3DG_ABLATE 0
+#endif
 
 namespace s3dg {
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kImgDw = 20;   // per-block LDS window image: pad,W1[8],pad,W2[8],pad,unused
 
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) {
     return (x << k) | (x >> (64 - k));
@@ -56,218 +63,211 @@ struct Xoshiro {
     }
 };
 
-// Byte masks over the dword at byte position p.
-__device__ __forceinline__ uint32_t keep_ge(int p, int e) {   // bytes with pos >= e
-    int t = e - p;
-    return t <= 0 ? 0xFFFFFFFFu : (t >= 4 ? 0u : (0xFFFFFFFFu << (8 * t)));
-}
-__device__ __forceinline__ uint32_t keep_lt(int p, int e) {   // bytes with pos < e
-    int t = e - p;
-    return t <= 0 ? 0u : (t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * t)) - 1u));
-}
-
-// Dword of a 32-byte window image starting at window-relative byte `rel`
-// (clamped to [-4, 32]; bytes outside the window are masked by the caller).
-__device__ __forceinline__ uint32_t window_dword(const uint32_t *img, int rel) {
-    rel = rel < -4 ? -4 : (rel > 32 ? 32 : rel);
-    const int idx = (rel + 4) >> 2;                 // 0..9 (img[0] is the pad)
-    const uint32_t d0 = img[idx], d1 = img[idx + 1];
-    return __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(rel & 3));
-}
-
-// Full byte-exact value of the dword at block byte p (slow path).
-__device__ __forceinline__ uint32_t patch_dword(uint32_t b, int p, int c, int m, int so,
-                                                bool w2, const uint32_t *img) {
-    uint32_t res = b & keep_ge(p, c);                          // zero prefix, :209-210
-    const uint32_t m1 = keep_ge(p, c) & keep_lt(p, c + m);     // first window, :217
-    res = (res & ~m1) | (window_dword(img, p - c) & m1);
-    if (w2) {                                                  // second window, :218-221
-        const uint32_t m2 = keep_ge(p, so) & keep_lt(p, so + m);
-        res = (res & ~m2) | (window_dword(img + 9, p - so) & m2);
-    }
-    return res;
-}
-
 template <bool NT>
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) {
     if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
-struct Tile {
-    uint8_t *dst;        // byte address of block `first`
-    uint64_t size;       // object size in bytes
-    uint64_t entropy;    // call_entropy of the object
-    uint32_t first;      // first block index (within the object)
-    uint32_t count;      // blocks in this tile, 1..64
-    PrefixParams pp;
+__device__ __forceinline__ uint32_t fastmod(uint32_t a, uint64_t M, uint32_t d) {
+    const uint64_t low = M * a;
+    return (uint32_t)__umul64hi(low, (uint64_t)d);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {   // SplitMix64 output function
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-workgroup LDS: the 4 KiB block image being assembled + its metadata.
+struct BlockLds {
+    uint8_t img[kBlk];
+    uint32_t meta[4];        // c, L
 };
 
-// One wave generates one tile.  `B` = this lane's 4 x 16 B of the base block
-// (bytes j*1024 + lane*16 .. +16), `img` = this wave's LDS image (64 x 20 dw).
-template <bool NT>
-__device__ __forceinline__ void run_tile(const Tile &T, const u32x4 (&B)[4], uint32_t *img,
-                                         uint32_t lane) {
-    // ---- phase 1: lane-parallel per-block parameters + PRNG ----------------
-    const bool valid = lane < T.count;
-    const uint32_t i = T.first + lane;
-    const uint32_t u = i % T.pp.unique;                                  // :201
-    const uint64_t off = (uint64_t)i * kBlk;
-    const uint32_t L = valid ? (uint32_t)((T.size - off) < kBlk ? (T.size - off) : kBlk) : 0u;
-    uint32_t cl = T.pp.floor_len;
-    if (T.pp.rem) {
-        const uint64_t r = T.pp.rem, d = T.pp.f_den;
-        cl += (uint32_t)(((uint64_t)(u + 1) * r) / d - ((uint64_t)u * r) / d);
-    }
-    const uint32_t c = cl < L ? cl : L;                                  // :209
-    const uint32_t m = (L - c) < kMod ? (L - c) : kMod;                  // :212-214
-    const uint32_t so = c > kHalf ? c : kHalf;                           // :218
-    const bool w2 = m > 0 && so + m <= L;                                // :219
+// Wave 0, phase 1: block parameters + PRNG chain.  Writes the metadata to LDS
+// (lane 0) and returns the window words in `w1`/`w2w` (wave-uniform).
+// Scalar-unit budget matters (one SALU per cycle per CU, ~365 cycles per
+// 4 KiB block at the write ceiling): the SplitMix64 expansion (all of the
+// 64-bit multiplies) runs on the VALU, one seed word per lane; only the 8
+// Xoshiro256++ steps (shifts/xors/adds) run on the scalar unit.
+struct Plan {
+    uint32_t c, L, m, so;
+    bool w2;
+    uint64_t w1[4], w2w[4];
+};
 
-    uint64_t x = (uint64_t)u + T.entropy;                                // :202
+__device__ __forceinline__ void plan_block(Plan &P, uint32_t lane, uint32_t i, uint64_t size,
+                                           uint64_t entropy, const PrefixParams &pp) {
+    const uint32_t u = pp.unique == 0xFFFFFFFFu ? i : fastmod(i, pp.m_unique, pp.unique);  // :201
+    const uint64_t off = (uint64_t)i * kBlk;
+    const uint32_t L = (uint32_t)((size - off) < kBlk ? (size - off) : kBlk);
+    uint32_t cl = pp.floor_len;
+    if (pp.rem) {                     // closed form of :177-190; period f_den in u
+        const uint32_t up = fastmod(u, pp.m_fden, pp.f_den);
+        const uint32_t r0 = pp.f_den <= 65536u ? fastmod(up * pp.rem, pp.m_fden, pp.f_den)
+                                               : (uint32_t)(((uint64_t)up * pp.rem) % pp.f_den);
+        cl += (uint32_t)((uint64_t)r0 + pp.rem >= pp.f_den);
+    }
+    P.L = L;
+    P.c = cl < L ? cl : L;                                               // :209
+    P.m = (L - P.c) < kMod ? (L - P.c) : kMod;                           // :212-214
+    P.so = P.c > kHalf ? P.c : kHalf;                                    // :218
+    P.w2 = P.m > 0 && P.so + P.m <= L;                                   // :219
+
+    // SmallRng::seed_from_u64(u + entropy) (:202-203): state word k =
+    // mix64(seed + (k+1)*phi) — lanes 0..3 compute one word each.
+    const uint64_t seed = (uint64_t)u + entropy;
+#if S3DG_ABLATE & 2
+    for (int q = 0; q < 4; ++q) { P.w1[q] = seed + q; P.w2w[q] = seed - q; }
+    return;
+#endif
+    const uint64_t zl = mix64(seed + (uint64_t)((lane & 3) + 1) * 0x9E3779B97F4A7C15ull);
     Xoshiro g;
-    g.s0 = splitmix_next(x);
-    g.s1 = splitmix_next(x);
-    g.s2 = splitmix_next(x);
-    g.s3 = splitmix_next(x);
+    g.s0 = readlane64(zl, 0);
+    g.s1 = readlane64(zl, 1);
+    g.s2 = readlane64(zl, 2);
+    g.s3 = readlane64(zl, 3);
     uint64_t r[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) r[q] = g.next();
-    // fill_bytes_via_next: k1 draws per window, last one >>32 if its tail is 1..4 B.
-    const uint32_t k1 = (m + 7) >> 3;
-    const uint32_t tail = m & 7;
-    const bool tail_hi = tail >= 1 && tail <= 4;
-    uint64_t w1[4], w2w[4];
+    if (P.m == kMod) {                // every full block with c <= 4064
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        w1[q] = r[q];
-        w2w[q] = k1 == 4 ? r[4 + q] : (k1 == 3 ? r[3 + q] : (k1 == 2 ? r[2 + q] : r[1 + q]));
-        if (tail_hi && (uint32_t)q + 1 == k1) { w1[q] >>= 32; w2w[q] >>= 32; }
-    }
-    uint32_t *mine = img + lane * kImgDw;
-    u32x4 *mv = reinterpret_cast<u32x4 *>(mine);
-    mv[0] = u32x4{0u, (uint32_t)w1[0], (uint32_t)(w1[0] >> 32), (uint32_t)w1[1]};
-    mv[1] = u32x4{(uint32_t)(w1[1] >> 32), (uint32_t)w1[2], (uint32_t)(w1[2] >> 32), (uint32_t)w1[3]};
-    mv[2] = u32x4{(uint32_t)(w1[3] >> 32), 0u, (uint32_t)w2w[0], (uint32_t)(w2w[0] >> 32)};
-    mv[3] = u32x4{(uint32_t)w2w[1], (uint32_t)(w2w[1] >> 32), (uint32_t)w2w[2], (uint32_t)(w2w[2] >> 32)};
-    mv[4] = u32x4{(uint32_t)w2w[3], (uint32_t)(w2w[3] >> 32), 0u, 0u};
-    const uint32_t meta0 = c | (so << 16);
-    const uint32_t meta1 = L | (m << 16) | ((uint32_t)w2 << 24);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ---- phase 2: the wave writes its blocks, 4 x 1 KiB stores each --------
-    const u32x4 zero = {0u, 0u, 0u, 0u};
-    for (uint32_t k = 0; k < T.count; ++k) {
-        const uint32_t a0 = __builtin_amdgcn_readlane(meta0, k);
-        const uint32_t a1 = __builtin_amdgcn_readlane(meta1, k);
-        const int bc = (int)(a0 & 0xFFFF), bso = (int)(a0 >> 16);
-        const int bL = (int)(a1 & 0xFFFF), bm = (int)((a1 >> 16) & 0xFF);
-        const bool bw2 = (a1 >> 24) != 0;
-        uint8_t *bd = T.dst + (uint64_t)k * kBlk;
-        const uint32_t *bimg = img + k * kImgDw;
+        for (int q = 0; q < 4; ++q) { P.w1[q] = r[q]; P.w2w[q] = r[4 + q]; }
+    } else {
+        // fill_bytes_via_next on m < 32 bytes: k1 draws per window, the last
+        // one >>32 (next_u32) when its tail is 1..4 bytes
+        const uint32_t k1 = (P.m + 7) >> 3;
+        const uint32_t tail = P.m & 7;
+        const bool tail_hi = tail >= 1 && tail <= 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int o = j * 1024 + (int)lane * 16;
-            const bool need = (o < bc + bm && o + 16 > bc) ||
-                              (bw2 && o < bso + bm && o + 16 > bso) ||
-                              (o < bL && o + 16 > bL);
-            if (!need) {
-                if (o + 16 <= bL) store16<NT>(bd + o, (o + 16 <= bc) ? zero : B[j]);
-            } else {
-                u32x4 v;
-                v.x = patch_dword(B[j].x, o + 0, bc, bm, bso, bw2, bimg);
-                v.y = patch_dword(B[j].y, o + 4, bc, bm, bso, bw2, bimg);
-                v.z = patch_dword(B[j].z, o + 8, bc, bm, bso, bw2, bimg);
-                v.w = patch_dword(B[j].w, o + 12, bc, bm, bso, bw2, bimg);
-                if (o + 16 <= bL) {
-                    store16<NT>(bd + o, v);
-                } else {                       // ragged object tail: bytes < L only
-                    const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-                    for (int b = 0; b < 16 && o + b < bL; ++b)
-                        bd[o + b] = (uint8_t)(dw[b >> 2] >> (8 * (b & 3)));
-                }
-            }
+        for (int q = 0; q < 4; ++q) {
+            P.w1[q] = r[q];
+            P.w2w[q] = k1 == 4 ? r[4 + q] : (k1 == 3 ? r[3 + q] : (k1 == 2 ? r[2 + q] : r[1 + q]));
+            if (tail_hi && (uint32_t)q + 1 == k1) { P.w1[q] >>= 32; P.w2w[q] >>= 32; }
         }
     }
+}
+
+// Byte q (0..31) of a window given as 4 little-endian words.
+__device__ __forceinline__ uint8_t window_byte(const uint64_t (&w)[4], uint32_t q) {
+    const uint32_t k = (q >> 3) & 3;
+    const uint64_t x = k == 0 ? w[0] : (k == 1 ? w[1] : (k == 2 ? w[2] : w[3]));
+    return (uint8_t)(x >> (8 * (q & 7)));
+}
+
+// Wave 0, phase 2 (after every lane has copied the base block into the image):
+// zero bytes [c & ~15, c) of the partial segment, then window 1 at c, then
+// window 2 at so (later write wins, as :217-221).  One byte per lane.
+__device__ __forceinline__ void patch_image(BlockLds &S, const Plan &P, uint32_t lane) {
+    const uint32_t z0 = P.c & ~15u;
+    if (lane < P.c - z0) S.img[z0 + lane] = 0;                           // :209-210
+    if (lane < P.m) S.img[P.c + lane] = window_byte(P.w1, lane);         // :217
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if (P.w2 && lane < P.m) S.img[P.so + lane] = window_byte(P.w2w, lane);   // :219-221
 }
 
-__device__ __forceinline__ void load_base(const u32x4 *base, uint32_t lane, u32x4 (&B)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) B[j] = base[j * 64 + lane];
+// Every lane, phase 3: its 16 bytes at byte o of the block: zeros below c, else the image.
+template <bool NT>
+__device__ __forceinline__ void write_block(uint8_t *bd, const BlockLds &S, int o) {
+    const int c = (int)S.meta[0], L = (int)S.meta[1];
+    if (o >= L) return;
+    const u32x4 zero = {0u, 0u, 0u, 0u};
+    const u32x4 v = (o + 16 <= c) ? zero : *reinterpret_cast<const u32x4 *>(S.img + o);
+    if (o + 16 <= L) {
+        store16<NT>(bd + o, v);
+    } else {                                  // ragged object tail: bytes < L only
+        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+        for (int b = 0; b < 16 && o + b < L; ++b)
+            bd[o + b] = (uint8_t)(dw[b >> 2] >> (8 * (b & 3)));
+    }
 }
 
+// The whole per-block body (all three phases).
+template <bool NT>
+__device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, uint32_t wave,
+                                          uint32_t i, uint64_t size, uint64_t entropy,
+                                          const PrefixParams &pp, const u32x4 *base) {
+    const uint32_t lane = t & 63;
+    const u32x4 B = base[t];                       // bytes 16t..16t+15 of the base block
+    Plan P;
+    if (wave == 0) {
+        plan_block(P, lane, i, size, entropy, pp);
+        if (lane == 0) { S.meta[0] = P.c; S.meta[1] = P.L; }
+    }
+    *reinterpret_cast<u32x4 *>(S.img + 16 * t) = B;                   // :205-207
+    __syncthreads();
+#if !(S3DG_ABLATE & 1)
+    if (wave == 0) patch_image(S, P, lane);
+    __syncthreads();
+#endif
+    write_block<NT>(bd, S, (int)t * 16);
+}
+
+// Stream: blockIdx.x = block (blk_lo + x) of object (y0 + blockIdx.y).
 template <bool NT>
 __global__ __launch_bounds__(256) void k_fill_stream(uint8_t *dst, uint64_t obj_size,
-                                                     uint64_t stride, uint64_t n_objs,
-                                                     uint32_t blk_lo, uint32_t blk_hi,
-                                                     uint64_t seed_base, uint64_t first_obj,
-                                                     PrefixParams pp, const u32x4 *base) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kWavesPerWG * 64 * kImgDw];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    u32x4 B[4];
-    load_base(base, lane, B);
-    uint32_t *img = lds + wave * 64 * kImgDw;
-    const uint32_t span = blk_hi - blk_lo;
-    const uint64_t tpo = (span + kTileBlocks - 1) / kTileBlocks;
-    const uint64_t total = tpo * n_objs;
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerWG + wave; t < total; t += nw) {
-        const uint64_t j = t / tpo;
-        const uint32_t tin = (uint32_t)(t - j * tpo);
-        Tile T;
-        T.first = blk_lo + tin * kTileBlocks;
-        T.count = (blk_hi - T.first) < kTileBlocks ? (blk_hi - T.first) : kTileBlocks;
-        T.dst = dst + j * stride + (uint64_t)(T.first - blk_lo) * kBlk;
-        T.size = obj_size;
-        T.entropy = seed_base + ((first_obj + j) << 32);
-        T.pp = pp;
-        run_tile<NT>(T, B, img, lane);
-    }
+                                                     uint64_t stride, uint32_t blk_lo,
+                                                     uint64_t y0, uint64_t seed_base,
+                                                     uint64_t first_obj, PrefixParams pp,
+                                                     const u32x4 *base) {
+    __shared__ __attribute__((aligned(16))) BlockLds S;
+    const uint32_t t = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint64_t j = y0 + blockIdx.y;
+    uint64_t jv = j;                 // block address on the VALU: keep the scalar unit
+    asm volatile("" : "+v"(jv));     // for the PRNG chain
+    uint8_t *bd = dst + jv * stride + (uint64_t)blockIdx.x * kBlk;
+    gen_block<NT>(bd, S, t, wave, blk_lo + blockIdx.x, obj_size,
+                  seed_base + ((first_obj + j) << 32), pp, base);
 }
 
+// Batch: workgroup g -> tile g/64 -> object tab[tile_obj[g/64]], block
+// (g%64) + 64*(tile - tile_begin).  Tiles past an object's end exit.
 template <bool NT>
 __global__ __launch_bounds__(256) void k_fill_batch(uint8_t *dst_base, const ObjEntry *tab,
-                                                    uint64_t n, uint64_t total_tiles,
+                                                    const uint32_t *tile_obj, uint64_t g0,
                                                     const u32x4 *base) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kWavesPerWG * 64 * kImgDw];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    u32x4 B[4];
-    load_base(base, lane, B);
-    uint32_t *img = lds + wave * 64 * kImgDw;
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerWG + wave; t < total_tiles; t += nw) {
-        // largest e with tab[e].tile_begin <= t (wave-uniform search)
-        uint64_t lo = 0, hi = n;
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (tab[mid].tile_begin <= t) lo = mid; else hi = mid;
-        }
-        const ObjEntry e = tab[lo];
-        const uint32_t nb = (uint32_t)((e.size + kBlk - 1) / kBlk);
-        Tile T;
-        T.first = (uint32_t)(t - e.tile_begin) * kTileBlocks;
-        T.count = (nb - T.first) < kTileBlocks ? (nb - T.first) : kTileBlocks;
-        T.dst = dst_base + e.dst_off + (uint64_t)T.first * kBlk;
-        T.size = e.size;
-        T.entropy = e.entropy;
-        T.pp = e.pp;
-        run_tile<NT>(T, B, img, lane);
-    }
+    __shared__ __attribute__((aligned(16))) BlockLds S;
+    const uint32_t t = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint64_t g = g0 + blockIdx.x;
+    const uint64_t tile = g >> 6;
+    const ObjEntry e = tab[tile_obj[tile]];
+    const uint64_t ib = (tile - e.tile_begin) * kTileBlocks + (g & 63);
+    if (ib * kBlk >= e.size) return;               // uniform for the whole workgroup
+    gen_block<NT>(dst_base + e.dst_off + ib * kBlk, S, t, wave, (uint32_t)ib, e.size, e.entropy,
+                  e.pp, base);
 }
 
-template <bool NT>
-__global__ __launch_bounds__(256) void k_write_ceiling(uint8_t *dst, uint64_t n16, uint32_t pat) {
-    const u32x4 v = {pat, pat ^ 0x9E3779B9u, pat + 1u, ~pat};
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n16; q += stride)
-        store16<NT>(dst + q * 16, v);
+// tile_obj[tile] = object entry index, for every tile of every object.
+__global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t n,
+                                                  uint32_t *tile_obj) {
+    const uint64_t k = blockIdx.x;
+    if (k >= n) return;
+    const ObjEntry e = tab[k];
+    const uint64_t nt = ((e.size + kBlk - 1) / kBlk + kTileBlocks - 1) / kTileBlocks;
+    for (uint64_t q = threadIdx.x; q < nt; q += blockDim.x) tile_obj[e.tile_begin + q] = (uint32_t)k;
 }
+
+// Write-only ceiling in the same shape (one 4 KiB chunk per 256-thread workgroup).
+template <bool NT>
+__global__ __launch_bounds__(256) void k_write_ceiling(uint8_t *dst, uint64_t nchunks, uint64_t g0,
+                                                       uint32_t pat) {
+    const u32x4 v = {pat, pat ^ 0x9E3779B9u, pat + 1u, ~pat};
+    const uint64_t g = g0 + blockIdx.x;
+    if (g < nchunks) store16<NT>(dst + g * kBlk + threadIdx.x * 16, v);
+}
+
+constexpr uint64_t kMaxGridX = 1ull << 30;
 
 }  // namespace
 
@@ -276,37 +276,60 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               uint32_t blk_hi, uint64_t seed_base, uint64_t first_obj,
                               PrefixParams pp, const void *base_dev, hipStream_t s) {
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
-    if (lc.nontemporal)
-        hipLaunchKernelGGL(k_fill_stream<true>, dim3(lc.grid), dim3(256), 0, s, dst, obj_size,
-                           stride, n_objs, blk_lo, blk_hi, seed_base, first_obj, pp, b);
-    else
-        hipLaunchKernelGGL(k_fill_stream<false>, dim3(lc.grid), dim3(256), 0, s, dst, obj_size,
-                           stride, n_objs, blk_lo, blk_hi, seed_base, first_obj, pp, b);
-    return hipGetLastError();
+    const uint32_t nx = blk_hi - blk_lo;
+    for (uint64_t y0 = 0; y0 < n_objs; y0 += 65535) {
+        const uint32_t ny = (uint32_t)((n_objs - y0) < 65535 ? (n_objs - y0) : 65535);
+        for (uint64_t x0 = 0; x0 < nx; x0 += kMaxGridX) {
+            const uint32_t gx = (uint32_t)((nx - x0) < kMaxGridX ? (nx - x0) : kMaxGridX);
+            uint8_t *d = dst + x0 * kBlk;
+            if (lc.nontemporal)
+                hipLaunchKernelGGL(k_fill_stream<true>, dim3(gx, ny), dim3(256), 0, s, d, obj_size,
+                                   stride, (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
+            else
+                hipLaunchKernelGGL(k_fill_stream<false>, dim3(gx, ny), dim3(256), 0, s, d, obj_size,
+                                   stride, (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, const void *base_dev,
-                             hipStream_t s) {
+                             uint64_t n, uint64_t total_tiles, uint32_t *tile_obj,
+                             const void *base_dev, hipStream_t s) {
+    hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tile_obj);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
-    if (lc.nontemporal)
-        hipLaunchKernelGGL(k_fill_batch<true>, dim3(lc.grid), dim3(256), 0, s, dst_base, tab, n,
-                           total_tiles, b);
-    else
-        hipLaunchKernelGGL(k_fill_batch<false>, dim3(lc.grid), dim3(256), 0, s, dst_base, tab, n,
-                           total_tiles, b);
-    return hipGetLastError();
+    const uint64_t total = total_tiles * kTileBlocks;
+    for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
+        const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
+        if (lc.nontemporal)
+            hipLaunchKernelGGL(k_fill_batch<true>, dim3(gx), dim3(256), 0, s, dst_base, tab,
+                               tile_obj, g0, b);
+        else
+            hipLaunchKernelGGL(k_fill_batch<false>, dim3(gx), dim3(256), 0, s, dst_base, tab,
+                               tile_obj, g0, b);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len, uint32_t pattern,
                                 hipStream_t s) {
-    if (lc.nontemporal)
-        hipLaunchKernelGGL(k_write_ceiling<true>, dim3(lc.grid), dim3(256), 0, s, dst, len / 16,
-                           pattern);
-    else
-        hipLaunchKernelGGL(k_write_ceiling<false>, dim3(lc.grid), dim3(256), 0, s, dst, len / 16,
-                           pattern);
-    return hipGetLastError();
+    const uint64_t nch = len / kBlk;
+    for (uint64_t g0 = 0; g0 < nch; g0 += kMaxGridX) {
+        const uint32_t gx = (uint32_t)((nch - g0) < kMaxGridX ? (nch - g0) : kMaxGridX);
+        if (lc.nontemporal)
+            hipLaunchKernelGGL(k_write_ceiling<true>, dim3(gx), dim3(256), 0, s, dst, nch, g0, pattern);
+        else
+            hipLaunchKernelGGL(k_write_ceiling<false>, dim3(gx), dim3(256), 0, s, dst, nch, g0, pattern);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace s3dg

@@ -90,7 +90,7 @@ class Context:
     """One GPU's generator context (s3dg_ctx)."""
 
     def __init__(self, device: int = 0, base_block=None, base_seed: int | None = None,
-                 occupancy: int | None = None, nontemporal: bool = True):
+                 occupancy: int | None = None, nontemporal: bool = False):
         h = c_vp()
         call("s3dg_ctx_create", int(device), ctypes.byref(h))
         self._h = h

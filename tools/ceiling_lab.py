@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Run tools/ceiling_lab.hip variants interleaved in one process (tooling)."""
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_build", "libceiling_lab.so")
+
+
+def build():
+    os.makedirs(os.path.dirname(SO), exist_ok=True)
+    src = os.path.join(HERE, "ceiling_lab.hip")
+    if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
+                               "-shared", "-o", SO, src])
+
+
+def main():
+    build()
+    if "--build-only" in sys.argv:
+        return
+    import torch
+    L = ctypes.CDLL(SO)
+    gib = float(sys.argv[1]) if len(sys.argv) > 1 else 16
+    buf = torch.empty(int(gib * (1 << 30)), dtype=torch.uint8, device="cuda")
+    n = buf.numel()
+    p = buf.data_ptr()
+    st = torch.cuda.current_stream()
+    sh = st.cuda_stream
+    V = {}
+    base = torch.randint(0, 255, (4096,), dtype=torch.uint8, device="cuda")
+    bp = base.data_ptr()
+    V["v4 T=256 C=4096"] = lambda: L.lab_v4(ctypes.c_void_p(p), ctypes.c_uint64(n), ctypes.c_uint64(4096), 256, ctypes.c_void_p(sh))
+    V["v8 shared-chain T=256 (1D)"] = lambda: L.lab_v8(ctypes.c_void_p(p), ctypes.c_uint64(n), 256, ctypes.c_void_p(bp), ctypes.c_void_p(sh))
+    for nx in (2048, 256, 65536):
+        V[f"v9 shared-chain 2D nx={nx}"] = (lambda x=nx: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), x, 0, ctypes.c_void_p(bp), ctypes.c_void_p(sh)))
+        V[f"v10 ceiling 2D nx={nx}"] = (lambda x=nx: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), x, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh)))
+    V["torch fill_"] = lambda: buf.fill_(7)
+    res = {k: [] for k in V}
+    for _ in range(5):
+        for k, f in V.items():
+            f()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st); f(); e1.record(st)
+            torch.cuda.synchronize()
+            res[k].append(n / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    for k, v in res.items():
+        print(json.dumps({"variant": k, "GBps_median": round(statistics.median(v), 1), "max": round(max(v), 1)}))
+
+
+if __name__ == "__main__":
+    main()
