@@ -71,7 +71,7 @@ def parse():
     p.add_argument("--objects", type=int, default=None, help="override object count per rank")
     p.add_argument("--ring-gib", type=float, default=80.0,
                    help="device output ring per GPU (objects wrap when the step exceeds it)")
-    p.add_argument("--occupancy", type=int, default=None, help="workgroups per CU")
+    p.add_argument("--waves-per-block", type=int, default=None, help="1, 2 or 4 (default 2)")
     p.add_argument("--nt-stores", action="store_true", help="nontemporal stores (default plain)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -96,7 +96,7 @@ def main() -> int:
     dev = cp.local_rank
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
-    ctx = Context(dev, base_seed=BASE_SEED, occupancy=args.occupancy,
+    ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block,
                   nontemporal=args.nt_stores)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
@@ -251,7 +251,7 @@ def main() -> int:
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic_from_profiles(),
                          "kernel": "k_fill_stream" if cfg["size"] else "k_fill_batch",
-                         "launch_shape": "one 256-thread workgroup per 4 KiB block",
+                         "launch_shape": f"one {64 * (args.waves_per_block or 2)}-thread workgroup per 4 KiB block",
                          "avg_launch_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": int(sum(launch_bytes) / len(launch_bytes)),
                          "write_ceiling_GBps": round(ceiling_gbs, 1),

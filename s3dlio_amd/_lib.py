@@ -46,7 +46,7 @@ SIGNATURES = {
     "s3dg_set_base_block": (c_int, [c_vp, c_u8p]),
     "s3dg_set_base_block_seed": (c_int, [c_vp, c_u64]),
     "s3dg_get_base_block": (c_int, [c_vp, c_u8p]),
-    "s3dg_set_occupancy": (c_int, [c_vp, c_int]),
+    "s3dg_set_waves_per_block": (c_int, [c_vp, c_int]),
     "s3dg_set_nontemporal": (c_int, [c_vp, c_int]),
     "s3dg_unique_blocks": (c_u64, [c_u64, c_u64]),
     "s3dg_compress_ratio": (c_int, [c_u64, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]),

@@ -1,6 +1,8 @@
 """Build the C-ABI shared library libs3dlio_amd.so in-tree (gfx950 only).
 
-    python -m s3dlio_amd.build          # or __graft_entry__.build()
+    python s3dlio_amd/build.py          # or __graft_entry__.build()
+
+(run it by path: `python -m` would import the package, i.e. load the old .so)
 
 Plain hipcc, no CMake: two translation units (kernels + C ABI) linked into
 one .so that exports exactly the symbols of include/s3dlio_gpu.h.

@@ -22,6 +22,7 @@ using namespace s3dg;
 struct s3dg_ctx {
     int device = 0;
     bool nontemporal = false;          // plain stores measured faster
+    int waves_per_block = 2;           // measured best on MI355X
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // batch descriptor table (device) + pinned staging, grown on demand
@@ -101,6 +102,7 @@ int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den
 LaunchCfg cfg_for(s3dg_ctx *c) {
     LaunchCfg lc;
     lc.nontemporal = c->nontemporal;
+    lc.waves_per_block = c->waves_per_block;
     return lc;
 }
 
@@ -192,11 +194,11 @@ int s3dg_get_base_block(s3dg_ctx *c, uint8_t *out) {
     return S3DG_OK;
 }
 
-int s3dg_set_occupancy(s3dg_ctx *c, int wg_per_cu) {
-    // Kept for ABI stability: the kernels are non-persistent (one workgroup
-    // per 4 KiB block), so residency is left to the hardware dispatcher.
+int s3dg_set_waves_per_block(s3dg_ctx *c, int waves) {
     if (!c) return fail(S3DG_EINVAL, "null context");
-    if (wg_per_cu < 0 || wg_per_cu > 8) return fail(S3DG_EINVAL, "wg_per_cu must be 0..8");
+    if (waves == 0) waves = 2;
+    if (waves != 1 && waves != 2 && waves != 4) return fail(S3DG_EINVAL, "waves per block must be 1, 2 or 4");
+    c->waves_per_block = waves;
     return S3DG_OK;
 }
 

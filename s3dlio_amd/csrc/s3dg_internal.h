@@ -38,6 +38,7 @@ struct ObjEntry {
 
 struct LaunchCfg {
     bool nontemporal;
+    int waves_per_block;   // 1, 2 or 4 wave64s per 4 KiB block (one workgroup)
 };
 
 hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size,

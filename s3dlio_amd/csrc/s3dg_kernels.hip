@@ -29,6 +29,7 @@
 #define S3DG_ABLATE 0
 #endif
 
+
 namespace s3dg {
 namespace {
 
@@ -129,12 +130,22 @@ __device__ __forceinline__ void plan_block(Plan &P, uint32_t lane, uint32_t i, u
     for (int q = 0; q < 4; ++q) { P.w1[q] = seed + q; P.w2w[q] = seed - q; }
     return;
 #endif
-    const uint64_t zl = mix64(seed + (uint64_t)((lane & 3) + 1) * 0x9E3779B97F4A7C15ull);
     Xoshiro g;
+#if S3DG_ABLATE & 16
+    g.s0 = mix64(seed + 1 * 0x9E3779B97F4A7C15ull);
+    g.s1 = mix64(seed + 2 * 0x9E3779B97F4A7C15ull);
+    g.s2 = mix64(seed + 3 * 0x9E3779B97F4A7C15ull);
+    g.s3 = mix64(seed + 4 * 0x9E3779B97F4A7C15ull);
+#else
+    const uint64_t zl = mix64(seed + (uint64_t)((lane & 3) + 1) * 0x9E3779B97F4A7C15ull);
     g.s0 = readlane64(zl, 0);
     g.s1 = readlane64(zl, 1);
     g.s2 = readlane64(zl, 2);
     g.s3 = readlane64(zl, 3);
+#endif
+#if S3DG_ABLATE & 8
+    asm volatile("" : "+v"(g.s0), "+v"(g.s1), "+v"(g.s2), "+v"(g.s3));
+#endif
     uint64_t r[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) r[q] = g.next();
@@ -191,30 +202,36 @@ __device__ __forceinline__ void write_block(uint8_t *bd, const BlockLds &S, int 
     }
 }
 
-// The whole per-block body (all three phases).
-template <bool NT>
+// The whole per-block body (all three phases); NW waves per 4 KiB block.
+template <bool NT, int NW>
 __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, uint32_t wave,
                                           uint32_t i, uint64_t size, uint64_t entropy,
                                           const PrefixParams &pp, const u32x4 *base) {
+    constexpr int T = 64 * NW, SPL = 4 / NW;   // segments per lane
     const uint32_t lane = t & 63;
-    const u32x4 B = base[t];                       // bytes 16t..16t+15 of the base block
+    u32x4 B[SPL];
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) B[k] = base[t + k * T];   // bytes 16(t+kT).. of the base block
     Plan P;
     if (wave == 0) {
         plan_block(P, lane, i, size, entropy, pp);
         if (lane == 0) { S.meta[0] = P.c; S.meta[1] = P.L; }
     }
-    *reinterpret_cast<u32x4 *>(S.img + 16 * t) = B;                   // :205-207
+#pragma unroll
+    for (int k = 0; k < SPL; ++k)
+        *reinterpret_cast<u32x4 *>(S.img + 16 * (t + k * T)) = B[k];   // :205-207
     __syncthreads();
 #if !(S3DG_ABLATE & 1)
     if (wave == 0) patch_image(S, P, lane);
     __syncthreads();
 #endif
-    write_block<NT>(bd, S, (int)t * 16);
+#pragma unroll
+    for (int k = 0; k < SPL; ++k) write_block<NT>(bd, S, (int)(t + k * T) * 16);
 }
 
 // Stream: blockIdx.x = block (blk_lo + x) of object (y0 + blockIdx.y).
-template <bool NT>
-__global__ __launch_bounds__(256) void k_fill_stream(uint8_t *dst, uint64_t obj_size,
+template <bool NT, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t obj_size,
                                                      uint64_t stride, uint32_t blk_lo,
                                                      uint64_t y0, uint64_t seed_base,
                                                      uint64_t first_obj, PrefixParams pp,
@@ -226,14 +243,14 @@ __global__ __launch_bounds__(256) void k_fill_stream(uint8_t *dst, uint64_t obj_
     uint64_t jv = j;                 // block address on the VALU: keep the scalar unit
     asm volatile("" : "+v"(jv));     // for the PRNG chain
     uint8_t *bd = dst + jv * stride + (uint64_t)blockIdx.x * kBlk;
-    gen_block<NT>(bd, S, t, wave, blk_lo + blockIdx.x, obj_size,
+    gen_block<NT, NW>(bd, S, t, wave, blk_lo + blockIdx.x, obj_size,
                   seed_base + ((first_obj + j) << 32), pp, base);
 }
 
 // Batch: workgroup g -> tile g/64 -> object tab[tile_obj[g/64]], block
 // (g%64) + 64*(tile - tile_begin).  Tiles past an object's end exit.
-template <bool NT>
-__global__ __launch_bounds__(256) void k_fill_batch(uint8_t *dst_base, const ObjEntry *tab,
+template <bool NT, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const ObjEntry *tab,
                                                     const uint32_t *tile_obj, uint64_t g0,
                                                     const u32x4 *base) {
     __shared__ __attribute__((aligned(16))) BlockLds S;
@@ -244,7 +261,7 @@ __global__ __launch_bounds__(256) void k_fill_batch(uint8_t *dst_base, const Obj
     const ObjEntry e = tab[tile_obj[tile]];
     const uint64_t ib = (tile - e.tile_begin) * kTileBlocks + (g & 63);
     if (ib * kBlk >= e.size) return;               // uniform for the whole workgroup
-    gen_block<NT>(dst_base + e.dst_off + ib * kBlk, S, t, wave, (uint32_t)ib, e.size, e.entropy,
+    gen_block<NT, NW>(dst_base + e.dst_off + ib * kBlk, S, t, wave, (uint32_t)ib, e.size, e.entropy,
                   e.pp, base);
 }
 
@@ -269,6 +286,33 @@ __global__ __launch_bounds__(256) void k_write_ceiling(uint8_t *dst, uint64_t nc
 
 constexpr uint64_t kMaxGridX = 1ull << 30;
 
+template <bool NT, int NW>
+void launch_stream_one(dim3 g, hipStream_t s, uint8_t *d, uint64_t obj_size, uint64_t stride,
+                       uint32_t blk_lo, uint64_t y0, uint64_t seed_base, uint64_t first_obj,
+                       PrefixParams pp, const u32x4 *b) {
+    hipLaunchKernelGGL((k_fill_stream<NT, NW>), g, dim3(64 * NW), 0, s, d, obj_size, stride, blk_lo,
+                       y0, seed_base, first_obj, pp, b);
+}
+
+template <bool NT, int NW>
+void launch_batch_one(dim3 g, hipStream_t s, uint8_t *d, const ObjEntry *tab,
+                      const uint32_t *tile_obj, uint64_t g0, const u32x4 *b) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), 0, s, d, tab, tile_obj, g0, b);
+}
+
+#define S3DG_DISPATCH(fn, lc, ...)                                              \
+    do {                                                                        \
+        if (lc.nontemporal) {                                                   \
+            if (lc.waves_per_block == 1) fn<true, 1>(__VA_ARGS__);              \
+            else if (lc.waves_per_block == 4) fn<true, 4>(__VA_ARGS__);         \
+            else fn<true, 2>(__VA_ARGS__);                                      \
+        } else {                                                                \
+            if (lc.waves_per_block == 1) fn<false, 1>(__VA_ARGS__);             \
+            else if (lc.waves_per_block == 4) fn<false, 4>(__VA_ARGS__);        \
+            else fn<false, 2>(__VA_ARGS__);                                     \
+        }                                                                       \
+    } while (0)
+
 }  // namespace
 
 hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size,
@@ -281,13 +325,8 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
         const uint32_t ny = (uint32_t)((n_objs - y0) < 65535 ? (n_objs - y0) : 65535);
         for (uint64_t x0 = 0; x0 < nx; x0 += kMaxGridX) {
             const uint32_t gx = (uint32_t)((nx - x0) < kMaxGridX ? (nx - x0) : kMaxGridX);
-            uint8_t *d = dst + x0 * kBlk;
-            if (lc.nontemporal)
-                hipLaunchKernelGGL(k_fill_stream<true>, dim3(gx, ny), dim3(256), 0, s, d, obj_size,
-                                   stride, (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
-            else
-                hipLaunchKernelGGL(k_fill_stream<false>, dim3(gx, ny), dim3(256), 0, s, d, obj_size,
-                                   stride, (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
+            S3DG_DISPATCH(launch_stream_one, lc, dim3(gx, ny), s, dst + x0 * kBlk, obj_size, stride,
+                          (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -305,12 +344,7 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
     const uint64_t total = total_tiles * kTileBlocks;
     for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
-        if (lc.nontemporal)
-            hipLaunchKernelGGL(k_fill_batch<true>, dim3(gx), dim3(256), 0, s, dst_base, tab,
-                               tile_obj, g0, b);
-        else
-            hipLaunchKernelGGL(k_fill_batch<false>, dim3(gx), dim3(256), 0, s, dst_base, tab,
-                               tile_obj, g0, b);
+        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), s, dst_base, tab, tile_obj, g0, b);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -90,7 +90,7 @@ class Context:
     """One GPU's generator context (s3dg_ctx)."""
 
     def __init__(self, device: int = 0, base_block=None, base_seed: int | None = None,
-                 occupancy: int | None = None, nontemporal: bool = False):
+                 waves_per_block: int | None = None, nontemporal: bool = False):
         h = c_vp()
         call("s3dg_ctx_create", int(device), ctypes.byref(h))
         self._h = h
@@ -99,8 +99,8 @@ class Context:
             self.set_base_block(base_block)
         elif base_seed is not None:
             call("s3dg_set_base_block_seed", self._h, int(base_seed))
-        if occupancy is not None:
-            call("s3dg_set_occupancy", self._h, int(occupancy))
+        if waves_per_block is not None:
+            call("s3dg_set_waves_per_block", self._h, int(waves_per_block))
         call("s3dg_set_nontemporal", self._h, 1 if nontemporal else 0)
 
     # -- lifecycle -------------------------------------------------------------
@@ -134,8 +134,8 @@ class Context:
         call("s3dg_get_base_block", self._h, out.ctypes.data_as(_lib.c_u8p))
         return out.tobytes()
 
-    def set_occupancy(self, wg_per_cu: int) -> None:
-        call("s3dg_set_occupancy", self._h, int(wg_per_cu))
+    def set_waves_per_block(self, waves: int) -> None:
+        call("s3dg_set_waves_per_block", self._h, int(waves))
 
     def set_nontemporal(self, on: bool) -> None:
         call("s3dg_set_nontemporal", self._h, 1 if on else 0)

@@ -143,14 +143,14 @@ def test_store_modes_and_occupancy_agree(gpu_ctx, torch):
     ref = torch.empty(n * size, dtype=torch.uint8, device="cuda")
     gpu_ctx.fill_stream(ref, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
     for nt in (False, True):
-        for occ in (1, 2, 8):
+        for occ in (1, 2, 4):
             gpu_ctx.set_nontemporal(nt)
-            gpu_ctx.set_occupancy(occ)
+            gpu_ctx.set_waves_per_block(occ)
             t = torch.zeros_like(ref)
             gpu_ctx.fill_stream(t, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
             assert torch.equal(t, ref), (nt, occ)
-    gpu_ctx.set_nontemporal(True)
-    gpu_ctx.set_occupancy(0)
+    gpu_ctx.set_nontemporal(False)
+    gpu_ctx.set_waves_per_block(0)
 
 
 def test_host_dropin_seeded_multi_chunk(oracle, base):

@@ -6,16 +6,16 @@ import ctypes, json, os, statistics, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
-VARIANTS = [0, 1, 2, 3]
+VARIANTS = ["0", "2", "0 -DS3DG_NW=2", "2 -DS3DG_NW=2", "0 -DS3DG_NW=1", "2 -DS3DG_NW=1"]
 
 
 def build():
     os.makedirs(OUT, exist_ok=True)
     srcs = [os.path.join(ROOT, "s3dlio_amd", "csrc", f) for f in ("s3dg_kernels.hip", "s3dg_capi.cpp")]
     for k in VARIANTS:
-        so = os.path.join(OUT, f"libablate{k}.so")
+        so = os.path.join(OUT, f"libablate{k.replace(' ', '_').replace('=', '')}.so")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                               "-shared", f"-DS3DG_ABLATE={k}", "-I", os.path.join(ROOT, "include"),
+                               "-shared", *f"-DS3DG_ABLATE={k}".split(), "-I", os.path.join(ROOT, "include"),
                                "-I", os.path.join(ROOT, "s3dlio_amd", "csrc"), "-o", so] + srcs)
 
 
@@ -25,7 +25,7 @@ def main():
     import torch
     libs = {}
     for k in VARIANTS:
-        L = ctypes.CDLL(os.path.join(OUT, f"libablate{k}.so"), mode=os.RTLD_LOCAL)
+        L = ctypes.CDLL(os.path.join(OUT, f"libablate{k.replace(' ', '_').replace('=', '')}.so"), mode=os.RTLD_LOCAL)
         h = ctypes.c_void_p()
         assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
         libs[k] = (L, h)
