@@ -270,7 +270,7 @@ def traffic_from_profiles():
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get("write_bytes_per_launch")
+            return json.load(f).get("traffic_bytes_per_launch")
     except Exception:
         return None
 
