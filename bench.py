@@ -77,6 +77,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--device-override", type=int, default=None,
+                   help="rehearsal only: put every rank on this device (e.g. 2 ranks on a 1-GPU box)")
     return p.parse_args()
 
 
@@ -93,7 +95,7 @@ def main() -> int:
 
     cp = ControlPlane()
     rank, world = cp.rank, cp.world
-    dev = cp.local_rank
+    dev = cp.local_rank if args.device_override is None else args.device_override
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
     ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block,
