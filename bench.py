@@ -44,6 +44,9 @@ CONFIGS = {
             size=None, dedup=2, compress=(3, 2), scaling="weak"),
     5: dict(name="cfg5: 100000 x 8 MiB, dedup=2 compress=3 (total over all GPUs)", n=100000,
             size=8 * MiB, dedup=2, compress=3, scaling="strong"),
+    # not a BASELINE config: the K2 keystream (npz x-fill, npz.rs:376-383) over the cfg2 footprint
+    6: dict(name="k2: keystream fill, 10000 x 8 MiB as 2 MiB Xoshiro256++ chunks", n=10000,
+            size=8 * MiB, dedup=1, compress=1, scaling="weak", keystream=True),
 }
 
 
@@ -121,7 +124,13 @@ def main() -> int:
         stride = (size + 4095) // 4096 * 4096
         ring_objs = max(1, min(n_rank, ring_cap // stride))
         ring = torch.empty(ring_objs * stride, dtype=torch.uint8, device=f"cuda:{dev}")
-        for s0 in range(0, n_rank, ring_objs):
+        if cfg.get("keystream"):
+            # chunk index space continues across ranks: seed_base = first chunk of the rank
+            for s0 in range(0, n_rank, ring_objs):
+                k = min(ring_objs, n_rank - s0)
+                launches.append(("keystream", k * stride, (lo + s0) * stride // (2 * MiB)))
+                slot_obj = {t: (lo + s0 + t, size, t * stride) for t in range(k)}
+        for s0 in ([] if cfg.get("keystream") else range(0, n_rank, ring_objs)):
             k = min(ring_objs, n_rank - s0)
             launches.append(("stream", size, stride, k, lo + s0))
             for s in range(k):
@@ -155,7 +164,9 @@ def main() -> int:
             if evs is not None:
                 evs.append(torch.cuda.Event(enable_timing=True))
                 evs[-1].record(stream)
-            if L[0] == "stream":
+            if L[0] == "keystream":
+                call("s3dg_xoshiro_fill", ctx._h, base_ptr, L[1], 2 * MiB, L[2], sh)
+            elif L[0] == "stream":
                 _, size, stride, k, first = L
                 call("s3dg_fill_controlled_stream", ctx._h, base_ptr, size, stride, k,
                      cfg["dedup"], fn, fd, SEED_BASE, first, sh)
@@ -184,7 +195,7 @@ def main() -> int:
         per = [sum(L[1][k].size for k in range(L[2])) for L in launches]
         launch_bytes = per * args.steps
     elif len(launches) > 1:
-        per = [L[3] * L[1] for L in launches]
+        per = [L[1] if L[0] == "keystream" else L[3] * L[1] for L in launches]
         launch_bytes = per * args.steps
     avg_ms = sum(kern_ms) / len(kern_ms)
     achieved_gbs = sum(launch_bytes) / (sum(kern_ms) * 1e-3) / 1e9
@@ -204,6 +215,13 @@ def main() -> int:
         ok = True
         for s in sorted(pick):
             j, size, off = slot_obj[s]
+            if cfg.get("keystream"):
+                last = launches[-1]
+                chunk0 = last[2] + s * 4           # 4 x 2 MiB chunks per 8 MiB slot
+                got = ring[off:off + 2 * MiB].cpu().numpy()
+                exp = OC.xoshiro_chunks(2 * MiB, 2 * MiB, chunk0)
+                ok &= sha(got) == sha(exp)
+                continue
             got = ring[off:off + size].cpu().numpy()
             exp = OC.fill_controlled(size, cfg["dedup"], fn, fd, object_entropy(SEED_BASE, j), base)
             ok &= sha(got) == sha(exp)
@@ -251,9 +269,10 @@ def main() -> int:
                        "stores": "nontemporal" if args.nt_stores else "plain"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                         "traffic": traffic_from_profiles(),
-                         "kernel": "k_fill_stream" if cfg["size"] else "k_fill_batch",
-                         "launch_shape": f"one {64 * (args.waves_per_block or 2)}-thread workgroup per 4 KiB block",
+                         "traffic": traffic_from_profiles(args.config, int(sum(launch_bytes) / len(launch_bytes))),
+                         "kernel": "k_keystream" if cfg.get("keystream") else ("k_fill_stream" if cfg["size"] else "k_fill_batch"),
+                         "launch_shape": ("one wave per 2 MiB chunk (64 lanes x 4096 draws, jump-ahead)" if cfg.get("keystream")
+                                          else f"one {64 * (args.waves_per_block or 2)}-thread workgroup per 4 KiB block"),
                          "avg_launch_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": int(sum(launch_bytes) / len(launch_bytes)),
                          "write_ceiling_GBps": round(ceiling_gbs, 1),
@@ -267,14 +286,18 @@ def main() -> int:
     return 0
 
 
-def traffic_from_profiles():
-    """HBM bytes per launch from the committed PMC pass (profiles/), if any."""
+def traffic_from_profiles(config: int, launch_bytes: int):
+    """HBM bytes per launch from the committed PMC pass (profiles/traffic.json),
+    only when it was taken on this exact config and launch size."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get("traffic_bytes_per_launch")
+            t = json.load(f).get(str(config))
+        if t and t.get("algorithmic_bytes_per_launch") == launch_bytes:
+            return t.get("traffic_bytes_per_launch")
     except Exception:
-        return None
+        pass
+    return None
 
 
 def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=512, per_chunk=32):

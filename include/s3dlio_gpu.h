@@ -95,6 +95,15 @@ int s3dg_fill_controlled_stream(s3dg_ctx *ctx, void *dst, uint64_t obj_size,
 /* Mixed-size batch.  `descs` is a host array; it is copied before return. */
 int s3dg_fill_controlled_batch(s3dg_ctx *ctx, void *dst_base,
                                const s3dg_obj_desc *descs, uint64_t n, void *stream);
+/* Keystream fill (generate_npz_bytes_raw x-fill, src/data_formats/npz.rs:376-383):
+ * chunk k (chunk_bytes, last one ragged) of [dst, dst+len) =
+ * Xoshiro256PlusPlus::seed_from_u64(seed_base + k).fill_bytes(chunk).
+ * chunk_bytes: positive multiple of 128 (npz.rs uses 2 MiB). */
+int s3dg_xoshiro_fill(s3dg_ctx *ctx, void *dst, uint64_t len, uint64_t chunk_bytes,
+                      uint64_t seed_base, void *stream);
+/* Host helper: advance a Xoshiro256 state by n steps with the jump polynomial
+ * the kernels use (test/diagnostic; no GPU needed). */
+int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n);
 /* Write-only ceiling: fill `len` bytes with a constant using the same store
  * path (roofline denominator measured on the device). */
 int s3dg_write_ceiling(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern,

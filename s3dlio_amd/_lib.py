@@ -58,6 +58,8 @@ SIGNATURES = {
                                             c_u64, c_u64, c_vp]),
     "s3dg_fill_controlled_batch": (c_int, [c_vp, c_vp, ctypes.POINTER(ObjDesc), c_u64, c_vp]),
     "s3dg_write_ceiling": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
+    "s3dg_xoshiro_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_vp]),
+    "s3dg_xoshiro_jump": (c_int, [ctypes.POINTER(c_u64), c_u64]),
     "s3dg_device_alloc": (c_int, [c_vp, c_u64, ctypes.POINTER(c_vp)]),
     "s3dg_device_free": (c_int, [c_vp, c_vp]),
     "s3dg_host_alloc_pinned": (c_int, [c_u64, ctypes.POINTER(c_vp)]),

@@ -5,6 +5,7 @@
 // (:174-175).  No CPU generation path exists in this library: every byte is
 // produced by a HIP kernel, and a missing/failed GPU is an error.
 #include "s3dg_internal.h"
+#include "s3dg_jump.h"
 #include "s3dlio_gpu.h"
 
 #include <sys/random.h>
@@ -13,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -32,6 +34,7 @@ struct s3dg_ctx {
     uint32_t *tile_obj = nullptr;      // tile -> object entry map (device)
     uint64_t tile_cap = 0;
     hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
+    std::map<uint64_t, uint64_t *> jtabs;   // (lpc << 32 | span) -> device jump table
     std::mutex mu;
 };
 
@@ -167,6 +170,7 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     if (c->tab_dev) (void)hipFree(c->tab_dev);
     if (c->tab_host) (void)hipHostFree(c->tab_host);
     if (c->tile_obj) (void)hipFree(c->tile_obj);
+    for (auto &kv : c->jtabs) (void)hipFree(kv.second);
     if (c->tab_free) (void)hipEventDestroy(c->tab_free);
     delete c;
     return S3DG_OK;
@@ -289,6 +293,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         // only on its own stream, so drain the device before freeing
         HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
         if (c->tile_obj) (void)hipFree(c->tile_obj);
+    for (auto &kv : c->jtabs) (void)hipFree(kv.second);
         c->tile_obj = nullptr; c->tile_cap = 0;
         const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
         HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(uint32_t)), "hipMalloc(tile map)");
@@ -301,6 +306,47 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     HIP_TRY(launch_fill_batch(cfg_for(c), (uint8_t *)dst_base, c->tab_dev, m, tiles,
                               c->tile_obj, c->base_dev, s),
             "launch k_fill_batch");
+    return S3DG_OK;
+}
+
+int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
+    if (!state4) return fail(S3DG_EINVAL, "null state");
+    uint64_t J[4];
+    if (!jump_poly(n, J)) return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
+    apply_jump(state4, J);
+    return S3DG_OK;
+}
+
+int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes,
+                      uint64_t seed_base, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (len == 0) return S3DG_OK;
+    if (chunk_bytes == 0 || (chunk_bytes & 127u))
+        return fail(S3DG_EINVAL, "chunk_bytes must be a positive multiple of 128");
+    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    // lanes per chunk: as many as keep >= 2048 draws per lane (jump <= 12.5 %)
+    const uint64_t nd = chunk_bytes / 8;
+    uint32_t lpc = 1;
+    while (lpc < 64 && nd / (2 * lpc) >= 2048) lpc *= 2;
+    uint64_t span = (nd + lpc - 1) / lpc;
+    span = (span + 15) / 16 * 16;
+    if (span > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "chunk too large");
+    std::lock_guard<std::mutex> g(c->mu);
+    const uint64_t key = ((uint64_t)lpc << 32) | span;
+    auto it = c->jtabs.find(key);
+    if (it == c->jtabs.end()) {
+        std::vector<uint64_t> h(4 * 64, 0);
+        for (uint32_t k = 0; k < lpc; ++k)
+            if (!jump_poly((uint64_t)k * span, &h[4 * k]))
+                return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
+        uint64_t *d = nullptr;
+        HIP_TRY(hipMalloc(&d, h.size() * 8), "hipMalloc(jump table)");
+        HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(jump table)");
+        it = c->jtabs.emplace(key, d).first;
+    }
+    HIP_TRY(launch_keystream((uint8_t *)dst, len, chunk_bytes, seed_base, lpc, (uint32_t)span,
+                             it->second, (hipStream_t)stream),
+            "launch k_keystream");
     return S3DG_OK;
 }
 

@@ -50,6 +50,9 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
                              uint64_t n, uint64_t total_tiles, uint32_t *tile_obj,
                              const void *base_dev, hipStream_t s);
 
+hipError_t launch_keystream(uint8_t *dst, uint64_t len, uint64_t chunk_bytes, uint64_t seed_base,
+                           uint32_t lpc, uint32_t span, const uint64_t *jtab, hipStream_t s);
+
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
                                 uint32_t pattern, hipStream_t s);
 

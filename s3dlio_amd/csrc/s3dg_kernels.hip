@@ -284,6 +284,105 @@ __global__ __launch_bounds__(256) void k_write_ceiling(uint8_t *dst, uint64_t nc
     if (g < nchunks) store16<NT>(dst + g * kBlk + threadIdx.x * 16, v);
 }
 
+
+// ---------------------------------------------------------------------------
+// K2: keystream fill (generate_npz_bytes_raw x-fill, src/data_formats/npz.rs:376-383).
+// Chunk c (chunk_bytes each, last one ragged) of [dst, dst+len) =
+//   Xoshiro256PlusPlus::seed_from_u64(seed_base + c).fill_bytes(chunk).
+// `lpc` lanes share a chunk: lane `sub` starts at draw sub*span via the
+// jump polynomial jtab[sub] = x^(sub*span) mod P (s3dg_jump.cpp), 256 steps.
+// Each iteration a lane makes 16 draws (128 B) into its LDS row; the wave
+// then writes 8 rows' worth of whole 128-byte lines per store instruction
+// (8 lanes x 16 B per line), so every store covers full cache lines.
+constexpr int kRowStride = 144;   // 128 B + 16 B pad: conflict-light ds_write_b128 rows
+
+__device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2, uint64_t &s3) {
+    const uint64_t t = s1 << 17;
+    s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl64(s3, 45);
+}
+
+__global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, uint64_t len, uint64_t chunk_bytes,
+                                                  uint64_t nchunks, uint64_t seed_base, uint32_t lpc,
+                                                  uint32_t span, const uint64_t *jtab) {
+    __shared__ __attribute__((aligned(16))) uint8_t rows[4][64 * kRowStride];
+    const uint32_t t = threadIdx.x, l = t & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+    uint8_t *myrows = rows[w];
+    const uint32_t cpw = 64 / lpc;                                   // chunks per wave
+    const uint64_t c0 = ((uint64_t)blockIdx.x * 4 + w) * cpw;
+    const uint64_t c = c0 + l / lpc;
+    const uint32_t sub = l % lpc;
+    const uint64_t coff = c * chunk_bytes;
+    const uint64_t clen = c < nchunks ? ((len - coff) < chunk_bytes ? (len - coff) : chunk_bytes) : 0;
+    const uint64_t rb = (uint64_t)sub * span * 8;                    // lane region within chunk
+    const uint32_t rlen = (uint32_t)(clen > rb ? ((clen - rb) < (uint64_t)span * 8 ? (clen - rb) : (uint64_t)span * 8) : 0);
+    const uint64_t tail_draw = clen >> 3;                            // draw index of a 1..7 B tail
+    const bool tail_hi = (clen & 7) >= 1 && (clen & 7) <= 4;         // next_u32 = next_u64 >> 32
+
+    // seed_from_u64(seed_base + c) (npz.rs:381), then jump to draw sub*span
+    uint64_t x = seed_base + c;
+    uint64_t s0 = mix64(x + 0x9E3779B97F4A7C15ull), s1 = mix64(x + 2 * 0x9E3779B97F4A7C15ull);
+    uint64_t s2 = mix64(x + 3 * 0x9E3779B97F4A7C15ull), s3 = mix64(x + 4 * 0x9E3779B97F4A7C15ull);
+    if (lpc > 1 && sub > 0) {
+        const uint64_t *J = jtab + 4 * sub;
+        const uint64_t j0 = J[0], j1 = J[1], j2 = J[2], j3 = J[3];
+        uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        for (int i = 0; i < 256; ++i) {
+            const uint64_t jw = i < 64 ? j0 : (i < 128 ? j1 : (i < 192 ? j2 : j3));
+            const uint64_t msk = 0ull - ((jw >> (i & 63)) & 1ull);
+            a0 ^= s0 & msk; a1 ^= s1 & msk; a2 ^= s2 & msk; a3 ^= s3 & msk;
+            xo_step(s0, s1, s2, s3);
+        }
+        s0 = a0; s1 = a1; s2 = a2; s3 = a3;
+    }
+
+    // destination of the 8 rows this lane helps write: row 8i + l/8, piece l%8
+    const uint32_t piece = l & 7;
+    uint64_t raddr[8];
+    uint32_t rrem[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t r = 8 * i + (l >> 3);
+        raddr[i] = __shfl(coff + rb, (int)r);
+        rrem[i] = __shfl(rlen, (int)r);
+    }
+    const uint64_t d0 = (uint64_t)sub * span;                        // first draw index
+    const uint32_t iters = span / 16;
+    for (uint32_t it = 0; it < iters; ++it) {
+        // 16 draws -> this lane's LDS row
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+            uint64_t ra = rotl64(s0 + s3, 23) + s0; xo_step(s0, s1, s2, s3);
+            uint64_t rbv = rotl64(s0 + s3, 23) + s0; xo_step(s0, s1, s2, s3);
+            const uint64_t d = d0 + (uint64_t)it * 16 + q;
+            if (tail_hi && d == tail_draw) ra >>= 32;
+            if (tail_hi && d + 1 == tail_draw) rbv >>= 32;
+            *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
+                u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t o = it * 128 + piece * 16;                   // offset within the row's region
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t r = 8 * i + (l >> 3);
+            if (o >= rrem[i]) continue;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(myrows + r * kRowStride + piece * 16);
+            uint8_t *p = dst + raddr[i] + o;
+            if (o + 16 <= rrem[i]) {
+                *reinterpret_cast<u32x4 *>(p) = v;
+            } else {
+                const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+                for (uint32_t b = 0; b < 16 && o + b < rrem[i]; ++b) p[b] = (uint8_t)(dw[b >> 2] >> (8 * (b & 3)));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 constexpr uint64_t kMaxGridX = 1ull << 30;
 
 template <bool NT, int NW>
@@ -349,6 +448,18 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_keystream(uint8_t *dst, uint64_t len, uint64_t chunk_bytes, uint64_t seed_base,
+                           uint32_t lpc, uint32_t span, const uint64_t *jtab, hipStream_t s) {
+    const uint64_t nchunks = (len + chunk_bytes - 1) / chunk_bytes;
+    const uint64_t cpw = 64 / lpc;
+    const uint64_t waves = (nchunks + cpw - 1) / cpw;
+    const uint64_t wgs = (waves + 3) / 4;
+    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_keystream, dim3((uint32_t)wgs), dim3(256), 0, s, dst, len, chunk_bytes,
+                       nchunks, seed_base, lpc, span, jtab);
+    return hipGetLastError();
 }
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len, uint32_t pattern,

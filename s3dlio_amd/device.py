@@ -175,6 +175,14 @@ class Context:
             arr[k] = ObjDesc(int(off), int(size), int(ent) & (2**64 - 1), int(dd), fn, fd)
         call("s3dg_fill_controlled_batch", self._h, _ptr(dst), arr, len(objs), _stream(stream))
 
+    def xoshiro_fill(self, dst, nbytes: int | None = None, chunk_bytes: int = 2 << 20,
+                     seed_base: int = 0, stream=None) -> None:
+        """Keystream fill, chunk k = Xoshiro256PlusPlus::seed_from_u64(seed_base + k)
+        .fill_bytes(chunk) (src/data_formats/npz.rs:376-383)."""
+        n = _nbytes(dst) if nbytes is None else nbytes
+        call("s3dg_xoshiro_fill", self._h, _ptr(dst), int(n), int(chunk_bytes),
+             int(seed_base) & (2**64 - 1), _stream(stream))
+
     def write_ceiling(self, dst, nbytes: int | None = None, pattern: int = 0xA5A5A5A5,
                       stream=None) -> None:
         n = _nbytes(dst) if nbytes is None else nbytes
@@ -182,6 +190,13 @@ class Context:
 
     def sync(self, stream=None) -> None:
         call("s3dg_sync", self._h, 0 if stream is None else _stream(stream))
+
+
+def xoshiro_jump(state, n: int) -> list[int]:
+    """Host jump-ahead of a Xoshiro256 state by n steps (the kernels' method)."""
+    s = (ctypes.c_uint64 * 4)(*[int(v) & (2**64 - 1) for v in state])
+    call("s3dg_xoshiro_jump", s, int(n))
+    return list(s)
 
 
 def device_count() -> int:

@@ -80,3 +80,17 @@ def test_version_string():
     from s3dlio_amd._lib import lib
     assert b"gfx950" in lib.s3dg_version()
     assert isinstance(ctypes.c_char_p(lib.s3dg_last_error()).value, (bytes, type(None)))
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 255, 4096, 8192, 262144 - 4096, 10**6])
+def test_host_jump_matches_stepping(n):
+    """Jump-ahead polynomial (s3dg_jump.cpp) == n sequential Xoshiro steps."""
+    from s3dlio_amd import xoshiro_jump
+    st = list(P.Xoshiro256pp.seed_from_u64(12345).s)
+    r = P.Xoshiro256pp(st)
+    if n <= 300000:
+        for _ in range(n):
+            r.next_u64()
+        assert xoshiro_jump(st, n) == r.s
+    else:   # composition: jump(n) == jump(n-a) after jump(a)
+        assert xoshiro_jump(xoshiro_jump(st, 4096), n - 4096) == xoshiro_jump(st, n)

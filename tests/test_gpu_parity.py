@@ -230,3 +230,41 @@ def test_invalid_arguments_raise(gpu_ctx, torch):
         gpu_ctx.fill_controlled(int(t.data_ptr()) + 1, 100)
     with pytest.raises(ValueError):
         gpu_ctx.fill_stream(t, obj_size=4096, n_objs=2, stride=100)
+
+
+def test_keystream_golden_fixtures(gpu_ctx, torch):
+    for c in load("xoshiro_chunks.json"):
+        t = torch.full((c["len"] + 64,), GUARD, dtype=torch.uint8, device="cuda")
+        gpu_ctx.xoshiro_fill(t, c["len"], chunk_bytes=c["chunk"], seed_base=c["seed_base"])
+        h = t.cpu().numpy()
+        assert sha(h[:c["len"]]) == c["sha256"], c
+        assert (h[c["len"]:] == GUARD).all()
+
+
+@pytest.mark.parametrize("length,chunk,sb", [
+    (64 * 2**20 + 5, 2 * 2**20, 0),        # npz.rs chunking, ragged 1..4-byte tail
+    (3 * 2**20 + 6, 2 * 2**20, 9),         # 5..7-byte tail
+    (2**20 + 4, 256 * 1024, 3),
+    (10 * 1152 + 7, 1152, 77),             # one lane per chunk
+    (2 * 2**20 + 128, 2 * 2**20 + 128, 1),
+    (1, 128, 0),
+])
+def test_keystream_vs_oracle(gpu_ctx, torch, oracle, length, chunk, sb):
+    t = torch.full((length + 64,), GUARD, dtype=torch.uint8, device="cuda")
+    gpu_ctx.xoshiro_fill(t, length, chunk_bytes=chunk, seed_base=sb)
+    h = t.cpu().numpy()
+    exp = oracle.xoshiro_chunks(length, chunk, sb)
+    assert np.array_equal(h[:length], exp)
+    assert (h[length:] == GUARD).all()
+
+
+def test_keystream_full_size_properties(gpu_ctx, torch, oracle):
+    """8 GiB of 2 MiB chunks: sampled chunks bit-exact, bytes ~uniform."""
+    n = 8 * 2**30
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu_ctx.xoshiro_fill(t, chunk_bytes=2 * 2**20, seed_base=0)
+    for k in (0, 1, 1000, 4095):
+        exp = oracle.xoshiro_chunks(2 * 2**20, 2 * 2**20, k)
+        assert np.array_equal(t[k * 2**21:(k + 1) * 2**21].cpu().numpy(), exp), k
+    hist = torch.bincount(t[:2**30].to(torch.int32), minlength=256).double()
+    assert float((hist.max() - hist.min()) / hist.mean()) < 0.01
