@@ -101,6 +101,14 @@ int s3dg_fill_controlled_batch(s3dg_ctx *ctx, void *dst_base,
  * chunk_bytes: positive multiple of 128 (npz.rs uses 2 MiB). */
 int s3dg_xoshiro_fill(s3dg_ctx *ctx, void *dst, uint64_t len, uint64_t chunk_bytes,
                       uint64_t seed_base, void *stream);
+/* dgen-contract object ("DG1"): 1 MiB blocks [blk_lo, blk_hi) of
+ * an obj_size-byte object, block blk_lo at dst.  Block i = Xoshiro256++ seeded
+ * seed ^ ((i % U) * 0x9E3779B97F4A7C15) (U = s3dg_unique_blocks), its first
+ * floor(L * f_num / f_den) bytes zero.  Behind DataGenerator/ObjectGen
+ * (src/data_gen.rs:253-371) and dgen's generate_data; parity unpinned. */
+int s3dg_dgen_fill(s3dg_ctx *ctx, void *dst, uint64_t obj_size, uint64_t blk_lo,
+                   uint64_t blk_hi, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                   uint64_t seed, void *stream);
 /* Host helper: advance a Xoshiro256 state by n steps with the jump polynomial
  * the kernels use (test/diagnostic; no GPU needed). */
 int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n);
@@ -120,6 +128,31 @@ int s3dg_stream_create(s3dg_ctx *ctx, void **out);
 int s3dg_stream_destroy(s3dg_ctx *ctx, void *stream);
 int s3dg_sync(s3dg_ctx *ctx, void *stream);   /* stream NULL: whole device */
 int s3dg_device_count(int *out);
+
+/* ---- streaming generator (DataGenerator / ObjectGen / PyO3 Generator) ----- */
+/* One object of `size` bytes in the DG1 layout, generated on the default
+ * context's GPU and streamed into host buffers.  has_seed=0: time + counter
+ * entropy like DataGenerator::new(None) (src/data_gen.rs:271-291).
+ * compress/dedup 0 are treated as 1 (src/data_gen_alt.rs:108-109). */
+typedef struct s3dg_gen s3dg_gen;
+int s3dg_gen_create(uint64_t size, uint64_t dedup, uint64_t compress, int has_seed,
+                    uint64_t seed, s3dg_gen **out);
+int s3dg_gen_create_ratio(uint64_t size, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                          int has_seed, uint64_t seed, s3dg_gen **out);
+int s3dg_gen_destroy(s3dg_gen *gen);
+/* ObjectGenAlt::fill_chunk (src/data_gen_alt.rs:122): next min(cap, remaining)
+ * bytes into buf; *written = 0 once complete. */
+int s3dg_gen_fill_chunk(s3dg_gen *gen, uint8_t *buf, uint64_t cap, uint64_t *written);
+/* Random access: bytes [pos, pos+n) of the object (does not move position). */
+int s3dg_gen_fill_at(s3dg_gen *gen, uint8_t *buf, uint64_t pos, uint64_t n);
+int s3dg_gen_is_complete(s3dg_gen *gen);
+uint64_t s3dg_gen_position(s3dg_gen *gen);
+uint64_t s3dg_gen_total_size(s3dg_gen *gen);
+uint64_t s3dg_gen_seed(s3dg_gen *gen);
+int s3dg_gen_reset(s3dg_gen *gen);
+/* generate_data / generate_controlled_data_alt one-shot into buf. */
+int s3dg_generate_data(uint8_t *buf, uint64_t size, uint64_t dedup, uint64_t compress,
+                       int has_seed, uint64_t seed);
 
 /* ---- host-buffer drop-ins (src/data_gen.rs:151 signature) ---------------- */
 /* fill_controlled_data(buf, dedup, compress): time-based entropy and a

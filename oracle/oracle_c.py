@@ -55,6 +55,7 @@ def lib():
                                            u8p, ctypes.c_int]
         L.s3dgo_fill_stream_mt.restype = ctypes.c_int
         L.s3dgo_xoshiro_chunks.argtypes = [u8p, u64, u64, u64]
+        L.s3dgo_dgen_fill.argtypes = [u8p, u64, u64, u64, u64, u64]
         _lib = L
     return _lib
 
@@ -121,4 +122,10 @@ def fill_stream(obj_size: int, n: int, dedup: int, f_num: int, f_den: int,
 def xoshiro_chunks(length: int, chunk: int, seed_base: int) -> np.ndarray:
     out = np.empty(length, np.uint8)
     lib().s3dgo_xoshiro_chunks(_ptr(out), length, chunk, seed_base)
+    return out
+
+
+def dgen_fill(size: int, dedup: int, f_num: int, f_den: int, seed: int) -> np.ndarray:
+    out = np.empty(size, np.uint8)
+    lib().s3dgo_dgen_fill(_ptr(out), size, dedup, f_num, f_den, seed & (2**64 - 1))
     return out

@@ -144,3 +144,18 @@ def xoshiro_chunks(length: int, chunk: int, seed_base: int) -> bytes:
         out += Xoshiro256pp.seed_from_u64((seed_base + k) & M64).fill_bytes(n)
         k += 1
     return bytes(out)
+
+
+def dgen_fill(size: int, dedup: int, f_num: int, f_den: int, seed: int) -> bytes:
+    """DG1 (build-defined dgen-contract layout): independent restatement."""
+    B = 1 << 20
+    nb = -(-size // B)
+    U = unique_blocks(nb, 1 if dedup == 0 else dedup)
+    out = bytearray()
+    for i in range(nb):
+        L = min(B, size - i * B)
+        blk = bytearray(Xoshiro256pp.seed_from_u64(seed ^ (((i % U) * 0x9E3779B97F4A7C15) & M64)).fill_bytes(L))
+        z = (L * f_num) // f_den
+        blk[:z] = bytes(z)
+        out += blk
+    return bytes(out)

@@ -240,3 +240,23 @@ void s3dgo_xoshiro_chunks(uint8_t *buf, uint64_t len, uint64_t chunk, uint64_t s
         s3dgo_fill_bytes(s, buf + off, n);
     }
 }
+
+/* ---- DG1: the build-defined dgen-contract layout --------- */
+/* Parity unpinned (dgen-data 0.2.4 is absent): this restates the build's own
+ * definition so the kernel is checked against an independent CPU version.
+ * 1 MiB blocks (DGEN_BLOCK_SIZE, src/constants.rs:348); block i =
+ * Xoshiro256++ seed_from_u64(seed ^ ((i % U) * phi)).fill_bytes(L), first
+ * floor(L * f_num / f_den) bytes zero; U as src/data_gen.rs:162-167. */
+void s3dgo_dgen_fill(uint8_t *buf, uint64_t size, uint64_t dedup, uint64_t f_num,
+                     uint64_t f_den, uint64_t seed) {
+    const uint64_t B = 1ull << 20;
+    const uint64_t nb = (size + B - 1) / B;
+    const uint64_t U = s3dgo_unique_blocks(nb, dedup == 0 ? 1 : dedup);
+    for (uint64_t i = 0; i < nb; ++i) {
+        const uint64_t off = i * B, L = size - off < B ? size - off : B;
+        uint64_t s[4];
+        s3dgo_xoshiro_seed(s, seed ^ ((i % U) * 0x9E3779B97F4A7C15ull));
+        s3dgo_fill_bytes(s, buf + off, L);
+        memset(buf + off, 0, (L * f_num) / f_den);
+    }
+}

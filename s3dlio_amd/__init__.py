@@ -9,5 +9,10 @@ from ._lib import S3dgError, lib  # noqa: F401  (loads libs3dlio_amd.so)
 from .device import (BLOCK_SIZE, DEFAULT_BASE_SEED, Context, compress_ratio,  # noqa: F401
                      device_count, object_entropy, unique_blocks, xoshiro_jump)
 from .data_gen import fill_controlled_data, fill_controlled_data_seeded  # noqa: F401
+from .datagen import (DataGenerator, Generator, ObjectGen, default_data_gen_threads,  # noqa: F401
+                      generate_controlled_data_alt, generate_controlled_data_streaming,
+                      generate_data, generate_data_with_threads, generate_into_buffer,
+                      optimal_chunk_size, py_default_data_gen_threads, py_total_cpus,
+                      total_cpus)
 
 __version__ = "0.1.0"

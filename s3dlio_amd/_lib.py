@@ -60,6 +60,19 @@ SIGNATURES = {
     "s3dg_write_ceiling": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
     "s3dg_xoshiro_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_vp]),
     "s3dg_xoshiro_jump": (c_int, [ctypes.POINTER(c_u64), c_u64]),
+    "s3dg_dgen_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),
+    "s3dg_gen_create": (c_int, [c_u64, c_u64, c_u64, c_int, c_u64, ctypes.POINTER(c_vp)]),
+    "s3dg_gen_create_ratio": (c_int, [c_u64, c_u64, c_u32, c_u32, c_int, c_u64,
+                                      ctypes.POINTER(c_vp)]),
+    "s3dg_gen_destroy": (c_int, [c_vp]),
+    "s3dg_gen_fill_chunk": (c_int, [c_vp, c_vp, c_u64, ctypes.POINTER(c_u64)]),
+    "s3dg_gen_fill_at": (c_int, [c_vp, c_vp, c_u64, c_u64]),
+    "s3dg_gen_is_complete": (c_int, [c_vp]),
+    "s3dg_gen_position": (c_u64, [c_vp]),
+    "s3dg_gen_total_size": (c_u64, [c_vp]),
+    "s3dg_gen_seed": (c_u64, [c_vp]),
+    "s3dg_gen_reset": (c_int, [c_vp]),
+    "s3dg_generate_data": (c_int, [c_vp, c_u64, c_u64, c_u64, c_int, c_u64]),
     "s3dg_device_alloc": (c_int, [c_vp, c_u64, ctypes.POINTER(c_vp)]),
     "s3dg_device_free": (c_int, [c_vp, c_vp]),
     "s3dg_host_alloc_pinned": (c_int, [c_u64, ctypes.POINTER(c_vp)]),

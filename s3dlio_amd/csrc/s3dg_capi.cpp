@@ -317,20 +317,16 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
     return S3DG_OK;
 }
 
-int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes,
-                      uint64_t seed_base, void *stream) {
-    if (int r = check_ctx(c)) return r;
-    if (len == 0) return S3DG_OK;
-    if (chunk_bytes == 0 || (chunk_bytes & 127u))
-        return fail(S3DG_EINVAL, "chunk_bytes must be a positive multiple of 128");
-    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
-    // lanes per chunk: as many as keep >= 2048 draws per lane (jump <= 12.5 %)
+// lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
+static int keystream_plan(s3dg_ctx *c, uint64_t chunk_bytes, KeystreamArgs &A, const uint64_t **jtab) {
     const uint64_t nd = chunk_bytes / 8;
-    uint32_t lpc = 1;
+    uint32_t lpc = 1;   // as many lanes as keep >= 2048 draws per lane (jump cost <= 12.5 %)
     while (lpc < 64 && nd / (2 * lpc) >= 2048) lpc *= 2;
     uint64_t span = (nd + lpc - 1) / lpc;
     span = (span + 15) / 16 * 16;
     if (span > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "chunk too large");
+    A.lpc = lpc;
+    A.span = (uint32_t)span;
     std::lock_guard<std::mutex> g(c->mu);
     const uint64_t key = ((uint64_t)lpc << 32) | span;
     auto it = c->jtabs.find(key);
@@ -344,9 +340,59 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
         HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(jump table)");
         it = c->jtabs.emplace(key, d).first;
     }
-    HIP_TRY(launch_keystream((uint8_t *)dst, len, chunk_bytes, seed_base, lpc, (uint32_t)span,
-                             it->second, (hipStream_t)stream),
-            "launch k_keystream");
+    *jtab = it->second;
+    return S3DG_OK;
+}
+
+int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes,
+                      uint64_t seed_base, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (len == 0) return S3DG_OK;
+    if (chunk_bytes == 0 || (chunk_bytes & 127u))
+        return fail(S3DG_EINVAL, "chunk_bytes must be a positive multiple of 128");
+    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    KeystreamArgs A{};
+    const uint64_t *jt = nullptr;
+    if (int r = keystream_plan(c, chunk_bytes, A, &jt)) return r;
+    A.nchunks = (len + chunk_bytes - 1) / chunk_bytes;
+    A.chunk_bytes = chunk_bytes;
+    A.obj_len = len;
+    A.chunk0 = 0;
+    A.seed_base = seed_base;
+    A.seed_mode = 0;
+    A.unique = 0xFFFFFFFFu;
+    A.m_unique = 0;
+    A.zf_num = 0;
+    A.zf_den = 1;
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, (hipStream_t)stream), "launch k_keystream");
+    return S3DG_OK;
+}
+
+int s3dg_dgen_fill(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t blk_lo, uint64_t blk_hi,
+                   uint64_t dedup, uint32_t f_num, uint32_t f_den, uint64_t seed, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (obj_size == 0) return S3DG_OK;
+    const uint64_t nb = (obj_size + kDgenBlock - 1) / kDgenBlock;
+    if (blk_hi > nb) blk_hi = nb;
+    if (blk_lo >= blk_hi) return S3DG_OK;
+    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    if (f_den == 0 || f_num >= f_den) return fail(S3DG_EINVAL, "need f_num < f_den");
+    if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    KeystreamArgs A{};
+    const uint64_t *jt = nullptr;
+    if (int r = keystream_plan(c, kDgenBlock, A, &jt)) return r;
+    const uint64_t U = s3dg_unique_blocks(nb, dedup);
+    A.nchunks = blk_hi - blk_lo;
+    A.chunk_bytes = kDgenBlock;
+    A.obj_len = obj_size;
+    A.chunk0 = blk_lo;
+    A.seed_base = seed;
+    A.seed_mode = 1;
+    A.unique = U == nb ? 0xFFFFFFFFu : (uint32_t)U;
+    A.m_unique = fastmod_magic(U == nb ? 1u : (uint32_t)U);
+    A.zf_num = f_num;
+    A.zf_den = f_den;
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, (hipStream_t)stream), "launch k_keystream(dgen)");
     return S3DG_OK;
 }
 
@@ -485,6 +531,16 @@ uint64_t time_entropy() {      // SystemTime::now() ... as_nanos() as u64, :192-
 }  // namespace
 
 extern "C" {
+
+int s3dg_internal_fail(int code, const char *msg) { return fail(code, msg); }
+
+s3dg_ctx *s3dg_internal_default_ctx(int *err) {
+    DefaultCtx &D = dflt();
+    std::lock_guard<std::mutex> g(D.mu);
+    const int r = dflt_init(D);
+    if (err) *err = r;
+    return r ? nullptr : D.ctx;
+}
 
 int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress) {
     if (len == 0) return S3DG_OK;

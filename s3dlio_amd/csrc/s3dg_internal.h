@@ -8,6 +8,7 @@ namespace s3dg {
 constexpr uint32_t kBlk = 4096;   // BLK_SIZE   src/constants.rs:326
 constexpr uint32_t kHalf = 2048;  // HALF_BLK   src/constants.rs:329
 constexpr uint32_t kMod = 32;     // MOD_SIZE   src/constants.rs:352
+constexpr uint64_t kDgenBlock = 1ull << 20;   // DGEN_BLOCK_SIZE src/constants.rs:348
 constexpr uint32_t kTileBlocks = 64;  // blocks per batch tile (tile -> object map granule)
 constexpr int kWavesPerWG = 4;
 
@@ -50,8 +51,23 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
                              uint64_t n, uint64_t total_tiles, uint32_t *tile_obj,
                              const void *base_dev, hipStream_t s);
 
-hipError_t launch_keystream(uint8_t *dst, uint64_t len, uint64_t chunk_bytes, uint64_t seed_base,
-                           uint32_t lpc, uint32_t span, const uint64_t *jtab, hipStream_t s);
+// K2 keystream launch: chunks [chunk0, chunk0 + nchunks) of an obj_len-byte
+// object, chunk k at dst + (k - chunk0) * chunk_bytes.
+struct KeystreamArgs {
+    uint64_t nchunks;       // chunks in this launch
+    uint64_t chunk_bytes;
+    uint64_t obj_len;       // object size (sets the ragged last chunk)
+    uint64_t chunk0;        // first chunk index
+    uint64_t seed_base;
+    uint32_t seed_mode;     // 0: seed_base + k (npz.rs:381); 1: seed_base ^ ((k % U) * phi) (dgen mode)
+    uint32_t unique;        // U for seed_mode 1 (0xFFFFFFFF: none)
+    uint64_t m_unique;      // fastmod constant for U
+    uint64_t zf_num, zf_den;  // zero prefix = floor(chunk_len * zf_num / zf_den)
+    uint32_t lpc, span;     // lanes per chunk, draws per lane
+};
+
+hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
+                           hipStream_t s);
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
                                 uint32_t pattern, hipStream_t s);

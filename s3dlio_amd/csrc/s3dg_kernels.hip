@@ -301,29 +301,41 @@ __device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2
     s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl64(s3, 45);
 }
 
-__global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, uint64_t len, uint64_t chunk_bytes,
-                                                  uint64_t nchunks, uint64_t seed_base, uint32_t lpc,
-                                                  uint32_t span, const uint64_t *jtab) {
+__global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
     __shared__ __attribute__((aligned(16))) uint8_t rows[4][64 * kRowStride];
     const uint32_t t = threadIdx.x, l = t & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     uint8_t *myrows = rows[w];
+    const uint32_t lpc = A.lpc, span = A.span;
     const uint32_t cpw = 64 / lpc;                                   // chunks per wave
     const uint64_t c0 = ((uint64_t)blockIdx.x * 4 + w) * cpw;
-    const uint64_t c = c0 + l / lpc;
+    const uint64_t c = c0 + l / lpc;                                 // local chunk index
+    const uint64_t cg = A.chunk0 + c;                                // chunk index in the object
     const uint32_t sub = l % lpc;
-    const uint64_t coff = c * chunk_bytes;
-    const uint64_t clen = c < nchunks ? ((len - coff) < chunk_bytes ? (len - coff) : chunk_bytes) : 0;
+    const uint64_t coff = c * A.chunk_bytes;                         // offset within dst
+    const uint64_t gofs = cg * A.chunk_bytes;                        // offset within the object
+    const uint64_t clen = (c < A.nchunks && gofs < A.obj_len)
+                              ? ((A.obj_len - gofs) < A.chunk_bytes ? (A.obj_len - gofs) : A.chunk_bytes)
+                              : 0;
     const uint64_t rb = (uint64_t)sub * span * 8;                    // lane region within chunk
     const uint32_t rlen = (uint32_t)(clen > rb ? ((clen - rb) < (uint64_t)span * 8 ? (clen - rb) : (uint64_t)span * 8) : 0);
     const uint64_t tail_draw = clen >> 3;                            // draw index of a 1..7 B tail
     const bool tail_hi = (clen & 7) >= 1 && (clen & 7) <= 4;         // next_u32 = next_u64 >> 32
+    // zero prefix of the chunk (dgen-contract compressibility); 0 for the npz fill
+    const uint64_t zlen = A.zf_num ? (clen * A.zf_num) / A.zf_den : 0;
 
-    // seed_from_u64(seed_base + c) (npz.rs:381), then jump to draw sub*span
-    uint64_t x = seed_base + c;
+    // chunk seed: npz.rs:381 seed_from_u64(k), or the dgen mode
+    // seed ^ (u * phi) with u = chunk % U (dedup)
+    uint64_t x;
+    if (A.seed_mode == 0) {
+        x = A.seed_base + cg;
+    } else {
+        const uint32_t u = A.unique == 0xFFFFFFFFu ? (uint32_t)cg : fastmod((uint32_t)cg, A.m_unique, A.unique);
+        x = A.seed_base ^ ((uint64_t)u * 0x9E3779B97F4A7C15ull);
+    }
     uint64_t s0 = mix64(x + 0x9E3779B97F4A7C15ull), s1 = mix64(x + 2 * 0x9E3779B97F4A7C15ull);
     uint64_t s2 = mix64(x + 3 * 0x9E3779B97F4A7C15ull), s3 = mix64(x + 4 * 0x9E3779B97F4A7C15ull);
-    if (lpc > 1 && sub > 0) {
+    if (lpc > 1 && sub > 0) {                    // jump to draw sub*span
         const uint64_t *J = jtab + 4 * sub;
         const uint64_t j0 = J[0], j1 = J[1], j2 = J[2], j3 = J[3];
         uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -357,6 +369,8 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, uint64_t len, u
             const uint64_t d = d0 + (uint64_t)it * 16 + q;
             if (tail_hi && d == tail_draw) ra >>= 32;
             if (tail_hi && d + 1 == tail_draw) rbv >>= 32;
+            if (8 * d < zlen) ra &= (8 * d + 8 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d)));
+            if (8 * d + 8 < zlen) rbv &= (8 * d + 16 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d - 8)));
             *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
                 u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
         }
@@ -450,15 +464,13 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
     return hipSuccess;
 }
 
-hipError_t launch_keystream(uint8_t *dst, uint64_t len, uint64_t chunk_bytes, uint64_t seed_base,
-                           uint32_t lpc, uint32_t span, const uint64_t *jtab, hipStream_t s) {
-    const uint64_t nchunks = (len + chunk_bytes - 1) / chunk_bytes;
-    const uint64_t cpw = 64 / lpc;
-    const uint64_t waves = (nchunks + cpw - 1) / cpw;
+hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
+                           hipStream_t s) {
+    const uint64_t cpw = 64 / A.lpc;
+    const uint64_t waves = (A.nchunks + cpw - 1) / cpw;
     const uint64_t wgs = (waves + 3) / 4;
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_keystream, dim3((uint32_t)wgs), dim3(256), 0, s, dst, len, chunk_bytes,
-                       nchunks, seed_base, lpc, span, jtab);
+    hipLaunchKernelGGL(k_keystream, dim3((uint32_t)wgs), dim3(256), 0, s, dst, A, jtab);
     return hipGetLastError();
 }
 

@@ -183,6 +183,14 @@ class Context:
         call("s3dg_xoshiro_fill", self._h, _ptr(dst), int(n), int(chunk_bytes),
              int(seed_base) & (2**64 - 1), _stream(stream))
 
+    def dgen_fill(self, dst, obj_size: int, blk_lo: int = 0, blk_hi: int | None = None,
+                  dedup: int = 1, compress=1, seed: int = 0, stream=None) -> None:
+        """DG1 blocks [blk_lo, blk_hi) of an obj_size-byte object (1 MiB blocks)."""
+        fn, fd = compress_ratio(compress)
+        hi = (obj_size + (1 << 20) - 1) >> 20 if blk_hi is None else blk_hi
+        call("s3dg_dgen_fill", self._h, _ptr(dst), int(obj_size), int(blk_lo), int(hi),
+             int(dedup), fn, fd, int(seed) & (2**64 - 1), _stream(stream))
+
     def write_ceiling(self, dst, nbytes: int | None = None, pattern: int = 0xA5A5A5A5,
                       stream=None) -> None:
         n = _nbytes(dst) if nbytes is None else nbytes

@@ -94,3 +94,26 @@ def test_host_jump_matches_stepping(n):
         assert xoshiro_jump(st, n) == r.s
     else:   # composition: jump(n) == jump(n-a) after jump(a)
         assert xoshiro_jump(xoshiro_jump(st, 4096), n - 4096) == xoshiro_jump(st, n)
+
+
+def test_optimal_chunk_size_table():
+    """tests/test_optimal_chunking.rs:8-19."""
+    from s3dlio_amd import optimal_chunk_size
+    M = 1024 * 1024
+    for n, exp in [(10 * M, 10 * M), (16 * M, 16 * M), (20 * M, 16 * M), (32 * M, 32 * M),
+                   (50 * M, 32 * M), (64 * M, 64 * M), (100 * M, 64 * M), (1024 * M, 64 * M)]:
+        assert optimal_chunk_size(n) == exp
+
+
+def test_thread_count_utilities():
+    import os
+    import s3dlio_amd as S
+    assert S.py_total_cpus() == os.cpu_count()
+    assert 1 <= S.py_default_data_gen_threads() <= S.py_total_cpus()
+
+
+def test_dg1_oracles_agree():
+    from oracle import oracle_c as C
+    for (n, d, fn, fd, s) in [(3 * 2**20 + 5, 1, 0, 1, 7), (2**20 * 5 + 9, 2, 1, 2, 99),
+                              (100, 3, 2, 3, 5), (2**20, 1, 0, 1, 2**64 - 1), (7, 0, 1, 3, 1)]:
+        assert bytes(C.dgen_fill(n, d, fn, fd, s)) == P.dgen_fill(n, d, fn, fd, s)
