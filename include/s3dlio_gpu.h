@@ -129,6 +129,21 @@ int s3dg_stream_destroy(s3dg_ctx *ctx, void *stream);
 int s3dg_sync(s3dg_ctx *ctx, void *stream);   /* stream NULL: whole device */
 int s3dg_device_count(int *out);
 
+/* ---- CRC-32 and NPZ (src/data_formats/npz.rs:322-434) --------------------- */
+/* CRC-32 (IEEE, crc32fast / zlib.crc32) of dev[0, len); synchronous on `stream`. */
+int s3dg_crc32(s3dg_ctx *ctx, const void *dev, uint64_t len, void *stream, uint32_t *out);
+/* zlib crc32_combine: CRC of A||B from crc(A), crc(B), |B| (host). */
+uint32_t s3dg_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+/* Host CRC-32 update (crc32fast::Hasher semantics: start from 0). */
+uint32_t s3dg_crc32_host(uint32_t crc, const uint8_t *p, uint64_t n);
+/* Byte size of generate_npz_bytes_raw(shape, dtype, num_samples). */
+int s3dg_npz_size(const uint64_t *shape, int ndim, const char *dtype, uint64_t num_samples,
+                  uint64_t *total);
+/* generate_npz_bytes_raw into a host buffer of >= s3dg_npz_size bytes:
+ * byte-identical archive (x.npy keystream + CRC on the GPU, framing on host). */
+int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *dtype,
+                   uint64_t num_samples, uint8_t *out, uint64_t out_len);
+
 /* ---- streaming generator (DataGenerator / ObjectGen / PyO3 Generator) ----- */
 /* One object of `size` bytes in the DG1 layout, generated on the default
  * context's GPU and streamed into host buffers.  has_seed=0: time + counter

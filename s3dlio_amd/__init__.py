@@ -15,4 +15,6 @@ from .datagen import (DataGenerator, Generator, ObjectGen, default_data_gen_thre
                       optimal_chunk_size, py_default_data_gen_threads, py_total_cpus,
                       total_cpus)
 
+from .npz import crc32_combine, crc32_device, generate_npz_bytes, npz_size  # noqa: F401
+
 __version__ = "0.1.0"

@@ -73,6 +73,13 @@ SIGNATURES = {
     "s3dg_gen_seed": (c_u64, [c_vp]),
     "s3dg_gen_reset": (c_int, [c_vp]),
     "s3dg_generate_data": (c_int, [c_vp, c_u64, c_u64, c_u64, c_int, c_u64]),
+    "s3dg_crc32": (c_int, [c_vp, c_vp, c_u64, c_vp, ctypes.POINTER(c_u32)]),
+    "s3dg_crc32_combine": (c_u32, [c_u32, c_u32, c_u64]),
+    "s3dg_crc32_host": (c_u32, [c_u32, c_vp, c_u64]),
+    "s3dg_npz_size": (c_int, [ctypes.POINTER(c_u64), c_int, ctypes.c_char_p, c_u64,
+                              ctypes.POINTER(c_u64)]),
+    "s3dg_npz_build": (c_int, [c_vp, ctypes.POINTER(c_u64), c_int, ctypes.c_char_p, c_u64, c_vp,
+                               c_u64]),
     "s3dg_device_alloc": (c_int, [c_vp, c_u64, ctypes.POINTER(c_vp)]),
     "s3dg_device_free": (c_int, [c_vp, c_vp]),
     "s3dg_host_alloc_pinned": (c_int, [c_u64, ctypes.POINTER(c_vp)]),

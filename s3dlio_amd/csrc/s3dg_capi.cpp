@@ -6,6 +6,13 @@
 // produced by a HIP kernel, and a missing/failed GPU is an error.
 #include "s3dg_internal.h"
 #include "s3dg_jump.h"
+
+namespace s3dg {
+uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+uint32_t crc32_host_update(uint32_t crc, const uint8_t *p, uint64_t n);
+hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_t *out,
+                        void **tab_cache, uint32_t **seg_cache, uint64_t *seg_cap);
+}  // namespace s3dg
 #include "s3dlio_gpu.h"
 
 #include <sys/random.h>
@@ -35,6 +42,10 @@ struct s3dg_ctx {
     uint64_t tile_cap = 0;
     hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
     std::map<uint64_t, uint64_t *> jtabs;   // (lpc << 32 | span) -> device jump table
+    void *crc_tab = nullptr;           // slicing-by-8 tables (device)
+    uint32_t *crc_seg = nullptr;       // per-segment CRCs (device)
+    uint64_t crc_seg_cap = 0;
+    std::mutex crc_mu;
     std::mutex mu;
 };
 
@@ -171,6 +182,8 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     if (c->tab_host) (void)hipHostFree(c->tab_host);
     if (c->tile_obj) (void)hipFree(c->tile_obj);
     for (auto &kv : c->jtabs) (void)hipFree(kv.second);
+    if (c->crc_tab) (void)hipFree(c->crc_tab);
+    if (c->crc_seg) (void)hipFree(c->crc_seg);
     if (c->tab_free) (void)hipEventDestroy(c->tab_free);
     delete c;
     return S3DG_OK;
@@ -294,6 +307,8 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
         if (c->tile_obj) (void)hipFree(c->tile_obj);
     for (auto &kv : c->jtabs) (void)hipFree(kv.second);
+    if (c->crc_tab) (void)hipFree(c->crc_tab);
+    if (c->crc_seg) (void)hipFree(c->crc_seg);
         c->tile_obj = nullptr; c->tile_cap = 0;
         const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
         HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(uint32_t)), "hipMalloc(tile map)");
@@ -394,6 +409,29 @@ int s3dg_dgen_fill(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t blk_lo, u
     A.zf_den = f_den;
     HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, (hipStream_t)stream), "launch k_keystream(dgen)");
     return S3DG_OK;
+}
+
+int s3dg_crc32(s3dg_ctx *c, const void *dev, uint64_t len, void *stream, uint32_t *out) {
+    if (int r = check_ctx(c)) return r;
+    if (!out || (len && !dev)) return fail(S3DG_EINVAL, "null argument");
+    if (len && !aligned16(dev)) return fail(S3DG_EINVAL, "dev must be 16-byte aligned");
+    std::lock_guard<std::mutex> g(c->crc_mu);
+    HIP_TRY(crc32_device((const uint8_t *)dev, len, (hipStream_t)stream, out, &c->crc_tab, &c->crc_seg,
+                         &c->crc_seg_cap),
+            "crc32 kernel");
+    return S3DG_OK;
+}
+
+int s3dg_internal_crc_device(s3dg_ctx *c, const void *dev, uint64_t len, void *stream, uint32_t *out) {
+    return s3dg_crc32(c, dev, len, stream, out);
+}
+
+uint32_t s3dg_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+    return crc32_combine(crc1, crc2, len2);
+}
+
+uint32_t s3dg_crc32_host(uint32_t crc, const uint8_t *p, uint64_t n) {
+    return crc32_host_update(crc, p, n);
 }
 
 int s3dg_write_ceiling(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, void *stream) {
