@@ -6,22 +6,19 @@
 //
 // CRC is affine over GF(2), so pieces combine as in zlib's crc32_combine:
 //   crc(A || B) = multmodp(x^(8|B|) mod P, crc(A)) ^ crc(B).
-// Kernel: one 256-thread workgroup per segment of `seg_tiles` tiles of 16 KiB.
-// Lane l of a tile hashes bytes [64 l, 64 l + 64) (slicing-by-8, tables in
-// LDS), the 256 lane CRCs fold in a log-depth tree (shuffles within a wave,
-// LDS across waves) with one constant x^(8 * 64 * 2^k) per level, and the
-// workgroup folds its tiles in order.  The host folds the per-segment CRCs
-// and hashes the sub-tile tail itself.  Reads only: HBM-read bound.
+// Kernel: one wave per contiguous region (256 KiB by default), column-Horner
+// (k_crc32_regions); the host folds the region CRCs (table-driven constant
+// multiply) and hashes the sub-region tail itself.  Reads only: HBM-read bound.
 #include "s3dg_internal.h"
 
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 namespace s3dg {
 namespace {
 
 constexpr uint32_t kPoly = 0xEDB88320u;
-constexpr uint32_t kTile = 16384;       // bytes per tile = 256 lanes x 64 B
 
 __host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
     // a * b mod P in the reflected representation (x^0 = 0x80000000), as zlib
@@ -37,49 +34,56 @@ __host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
     return p;
 }
 
-struct CrcConsts {
-    uint32_t lvl[14];    // x^(8 * 64 * 2^k) mod P, k = 0..13 (64 B .. 512 KiB)
-    uint32_t tile;       // x^(8 * 16384)
+// Register-shift tables.  raw(M) is the CRC register after M from a zero
+// register (linear in M); A^k is "advance k zero bytes" = multmodp(x^(8k), .).
+//   Tbyte[k][x] = A^k(raw of the single byte x)     k = 0..15 (slicing-by-16)
+//   Trow[b][x]  = A^1024(x << 8b)                     (multiply by x^(8*1024))
+struct CrcTables {
+    uint32_t tbyte[16][256];
+    uint32_t trow[4][256];
 };
 
-__global__ __launch_bounds__(256) void k_crc32_segments(const uint8_t *src, uint64_t ntiles,
-                                                        uint32_t seg_tiles, const uint32_t *tables,
-                                                        CrcConsts K, uint32_t *seg_crc) {
-    __shared__ uint32_t T[8][256];
-    __shared__ uint32_t wred[4];
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (uint32_t k = t; k < 8 * 256; k += 256) (&T[0][0])[k] = tables[k];
-    __syncthreads();
-    const uint64_t tile0 = (uint64_t)blockIdx.x * seg_tiles;
-    uint32_t acc = 0;           // CRC of the segment so far (crc of empty = 0)
-    bool have = false;
-    for (uint32_t q = 0; q < seg_tiles && tile0 + q < ntiles; ++q) {
-        const uint32_t *p = reinterpret_cast<const uint32_t *>(src + (tile0 + q) * kTile + t * 64);
-        uint32_t c = 0xFFFFFFFFu;
-#pragma unroll
-        for (int k = 0; k < 16; k += 2) {            // slicing-by-8 over 64 bytes
-            const uint32_t a = p[k] ^ c, b = p[k + 1];
-            c = T[7][a & 0xFF] ^ T[6][(a >> 8) & 0xFF] ^ T[5][(a >> 16) & 0xFF] ^ T[4][a >> 24] ^
-                T[3][b & 0xFF] ^ T[2][(b >> 8) & 0xFF] ^ T[1][(b >> 16) & 0xFF] ^ T[0][b >> 24];
-        }
-        c ^= 0xFFFFFFFFu;
-        // fold lane pieces: level k merges pairs of 64*2^k-byte runs
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const uint32_t right = __shfl_down(c, 1u << k);
-            if ((lane & ((2u << k) - 1)) == 0) c = multmodp(K.lvl[k], c) ^ right;
-        }
-        if (lane == 0) wred[w] = c;                  // CRC of this wave's 4 KiB
-        __syncthreads();
-        if (t == 0) {
-            uint32_t tc = wred[0];
-            for (int k = 1; k < 4; ++k) tc = multmodp(K.lvl[6], tc) ^ wred[k];
-            acc = have ? multmodp(K.tile, acc) ^ tc : tc;
-            have = true;
-        }
-        __syncthreads();
+__device__ __forceinline__ uint32_t mul_row(const uint32_t (*T)[256], uint32_t v) {
+    return T[0][v & 0xFF] ^ T[1][(v >> 8) & 0xFF] ^ T[2][(v >> 16) & 0xFF] ^ T[3][v >> 24];
+}
+
+// One wave per region of `rows` 1 KiB rows (region = rows KiB, contiguous).
+// Lane l owns bytes [16 l, 16 l + 16) of every row: each row is one
+// coalesced 1 KiB load, and the lane keeps the Horner sum
+//   S_l = A^1024 S_l ^ raw16(piece)
+// so the region's raw CRC is XOR_l A^(16 (63 - l)) S_l.  Output: raw CRC per region.
+__global__ __launch_bounds__(256) void k_crc32_regions(const uint8_t *src, uint64_t nregions,
+                                                       uint32_t rows, const CrcTables *tabs,
+                                                       const uint32_t *lane_shift, uint32_t *out) {
+    __shared__ CrcTables T;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    {
+        const uint32_t *g = reinterpret_cast<const uint32_t *>(tabs);
+        uint32_t *d = reinterpret_cast<uint32_t *>(&T);
+        for (uint32_t k = t; k < sizeof(CrcTables) / 4; k += 256) d[k] = g[k];
     }
-    if (t == 0) seg_crc[blockIdx.x] = acc;
+    __syncthreads();
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (t >> 6);
+    if (r >= nregions) return;
+    const uint4 *p = reinterpret_cast<const uint4 *>(src + r * (uint64_t)rows * 1024) + lane;
+    uint32_t S = 0;
+    for (uint32_t row = 0; row < rows; row += 4) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = p[(row + k) * 64];     // 4 rows in flight
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+            uint32_t c = mul_row(T.trow, S);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) c ^= T.tbyte[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xFF];
+            S = c;
+        }
+    }
+    S = multmodp(lane_shift[lane], S);              // A^(16 (63 - lane))
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) S ^= __shfl_xor(S, k);
+    if (lane == 0) out[r] = S;
 }
 
 // x^(8 n) mod P (zlib x2nmodp(n, 3)) on the host.
@@ -98,6 +102,8 @@ uint32_t x8n(uint64_t n) {
 
 uint32_t crc_tables[8][256];
 bool tables_ready = false;
+CrcTables dev_tables_host;
+uint32_t lane_shift_host[64];
 
 void init_tables() {
     if (tables_ready) return;
@@ -109,6 +115,18 @@ void init_tables() {
     for (uint32_t n = 0; n < 256; ++n)
         for (int k = 1; k < 8; ++k)
             crc_tables[k][n] = (crc_tables[k - 1][n] >> 8) ^ crc_tables[0][crc_tables[k - 1][n] & 0xFF];
+    // raw CRC of one byte x is crc_tables[0][x]; A^k of it by k zero-byte steps
+    for (uint32_t x = 0; x < 256; ++x) {
+        uint32_t c = crc_tables[0][x];
+        for (int k = 0; k < 16; ++k) {
+            dev_tables_host.tbyte[k][x] = c;
+            c = (c >> 8) ^ crc_tables[0][c & 0xFF];
+        }
+    }
+    const uint32_t x1k = x8n(1024);
+    for (int b = 0; b < 4; ++b)
+        for (uint32_t x = 0; x < 256; ++x) dev_tables_host.trow[b][x] = multmodp(x1k, x << (8 * b));
+    for (int l = 0; l < 64; ++l) lane_shift_host[l] = x8n(16ull * (63 - l));
     tables_ready = true;
 }
 
@@ -125,56 +143,65 @@ uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
     return multmodp(x8n(len2), crc1) ^ crc2;
 }
 
-// CRC-32 of dev[0, len): device segments + host fold + host tail.
+// CRC-32 of dev[0, len): device regions (raw CRCs) + host fold + host tail.
+//   std(M) = ~(A^n(~0) ^ raw(M)),   raw(M1||M2) = A^|M2| raw(M1) ^ raw(M2)
 hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_t *out,
                         void **tab_cache, uint32_t **seg_cache, uint64_t *seg_cap) {
-    init_tables();
-    const uint64_t ntiles = len / kTile;
-    uint32_t crc = 0;
+    static std::mutex init_mu;
+    {
+        std::lock_guard<std::mutex> g(init_mu);
+        init_tables();
+    }
+    uint32_t rows = 256;                                  // 256 KiB per wave region
+    while (len / ((uint64_t)rows * 1024) > (1ull << 20)) rows *= 2;
+    const uint64_t region = (uint64_t)rows * 1024;
+    const uint64_t nreg = len / region;
+    uint32_t raw = 0;
     hipError_t e = hipSuccess;
-    if (ntiles) {
+    if (nreg) {
         if (!*tab_cache) {
-            if ((e = hipMalloc(tab_cache, sizeof(crc_tables))) != hipSuccess) return e;
-            if ((e = hipMemcpy(*tab_cache, crc_tables, sizeof(crc_tables), hipMemcpyHostToDevice)) != hipSuccess)
+            if ((e = hipMalloc(tab_cache, sizeof(CrcTables) + 64 * 4)) != hipSuccess) return e;
+            if ((e = hipMemcpy(*tab_cache, &dev_tables_host, sizeof(CrcTables), hipMemcpyHostToDevice)) != hipSuccess)
+                return e;
+            if ((e = hipMemcpy((uint8_t *)*tab_cache + sizeof(CrcTables), lane_shift_host, 64 * 4,
+                               hipMemcpyHostToDevice)) != hipSuccess)
                 return e;
         }
-        // ~8 tiles (128 KiB) per workgroup, at most 2^20 segments
-        uint32_t seg_tiles = 8;
-        while ((ntiles + seg_tiles - 1) / seg_tiles > (1u << 20)) seg_tiles *= 2;
-        const uint64_t nseg = (ntiles + seg_tiles - 1) / seg_tiles;
-        if (nseg > *seg_cap) {
+        if (nreg > *seg_cap) {
             if (*seg_cache) (void)hipFree(*seg_cache);
             *seg_cache = nullptr;
             *seg_cap = 0;
-            if ((e = hipMalloc(seg_cache, nseg * 4)) != hipSuccess) return e;
-            *seg_cap = nseg;
+            if ((e = hipMalloc(seg_cache, nreg * 4)) != hipSuccess) return e;
+            *seg_cap = nreg;
         }
-        CrcConsts K;
-        for (int k = 0; k < 14; ++k) K.lvl[k] = x8n(64ull << k);
-        K.tile = x8n(kTile);
-        hipLaunchKernelGGL(k_crc32_segments, dim3((uint32_t)nseg), dim3(256), 0, s, dev, ntiles,
-                           seg_tiles, (const uint32_t *)*tab_cache, K, *seg_cache);
+        const uint64_t wgs = (nreg + 3) / 4;
+        hipLaunchKernelGGL(k_crc32_regions, dim3((uint32_t)wgs), dim3(256), 0, s, dev, nreg, rows,
+                           (const CrcTables *)*tab_cache,
+                           (const uint32_t *)((uint8_t *)*tab_cache + sizeof(CrcTables)), *seg_cache);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        std::vector<uint32_t> h(nseg);
-        if ((e = hipMemcpyAsync(h.data(), *seg_cache, nseg * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        std::vector<uint32_t> h(nreg);
+        if ((e = hipMemcpyAsync(h.data(), *seg_cache, nreg * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        const uint64_t seg_bytes = (uint64_t)seg_tiles * kTile;
-        const uint32_t xseg = x8n(seg_bytes);
-        crc = h[0];
-        for (uint64_t k = 1; k < nseg; ++k) {
-            const uint64_t blen = (k + 1 < nseg) ? seg_bytes : (ntiles - k * seg_tiles) * kTile;
-            crc = multmodp(blen == seg_bytes ? xseg : x8n(blen), crc) ^ h[k];
-        }
+        // fold regions with a table-driven A^region multiply
+        const uint32_t xr = x8n(region);
+        uint32_t Tr[4][256];
+        for (int b = 0; b < 4; ++b)
+            for (uint32_t x = 0; x < 256; ++x) Tr[b][x] = multmodp(xr, x << (8 * b));
+        for (uint64_t k = 0; k < nreg; ++k)
+            raw = (Tr[0][raw & 0xFF] ^ Tr[1][(raw >> 8) & 0xFF] ^ Tr[2][(raw >> 16) & 0xFF] ^
+                   Tr[3][raw >> 24]) ^ h[k];
     }
-    const uint64_t tail = len - ntiles * kTile;
+    const uint64_t head = nreg * region;
+    uint32_t crc = nreg ? ~(multmodp(x8n(head), 0xFFFFFFFFu) ^ raw) : 0;
+    const uint64_t tail = len - head;
     if (tail) {
         std::vector<uint8_t> tb(tail);
-        if ((e = hipMemcpyAsync(tb.data(), dev + ntiles * kTile, tail, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        if ((e = hipMemcpyAsync(tb.data(), dev + head, tail, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        crc = ntiles ? crc32_combine(crc, crc32_host_update(0, tb.data(), tail), tail)
-                     : crc32_host_update(0, tb.data(), tail);
+        const uint32_t ct = crc32_host_update(0, tb.data(), tail);
+        crc = nreg ? crc32_combine(crc, ct, tail) : ct;
     }
     *out = crc;
     return hipSuccess;

@@ -22,17 +22,24 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 extern "C" int s3dg_internal_fail(int code, const char *msg);   // s3dg_capi.cpp
 extern "C" s3dg_ctx *s3dg_internal_default_ctx(int *err);       // s3dg_capi.cpp
+
+// Device staging for host-buffer generation: two 64 MiB chunks + two
+// streams.  Pooled process-wide so short-lived generators (generate_data on
+// small sizes) do not pay hipMalloc / stream creation per call.
+struct Scratch {
+    void *buf[2] = {nullptr, nullptr};
+    hipStream_t st[2] = {nullptr, nullptr};
+};
 
 struct s3dg_gen {
     s3dg_ctx *ctx = nullptr;
     uint64_t size = 0, dedup = 1, seed = 0, pos = 0;
     uint32_t f_num = 0, f_den = 1;
-    void *scratch[2] = {nullptr, nullptr};
-    hipStream_t st[2] = {nullptr, nullptr};
-    uint64_t scratch_blocks = 0;
+    Scratch *sc = nullptr;
     std::mutex mu;
 };
 
@@ -58,15 +65,41 @@ uint64_t unseeded_entropy() {
             return s3dg_internal_fail(S3DG_EHIP, (std::string(what) + ": " + hipGetErrorString(e_)).c_str()); \
     } while (0)
 
-int ensure_scratch(s3dg_gen *g) {
-    if (g->scratch[0]) return S3DG_OK;
-    const uint64_t nb = (g->size + kDgenBlock - 1) / kDgenBlock;
-    g->scratch_blocks = nb < kMaxScratchBlocks ? nb : kMaxScratchBlocks;
-    for (int k = 0; k < 2; ++k) {
-        GEN_HIP(hipMalloc(&g->scratch[k], g->scratch_blocks * kDgenBlock), "hipMalloc(generator scratch)");
-        GEN_HIP(hipStreamCreateWithFlags(&g->st[k], hipStreamNonBlocking), "hipStreamCreate");
+std::mutex pool_mu;
+std::vector<Scratch *> pool;    // idle scratch sets
+
+int acquire_scratch(s3dg_gen *g) {
+    if (g->sc) return S3DG_OK;
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        if (!pool.empty()) {
+            g->sc = pool.back();
+            pool.pop_back();
+            return S3DG_OK;
+        }
     }
+    Scratch *sc = new Scratch();
+    for (int k = 0; k < 2; ++k) {
+        if (hipMalloc(&sc->buf[k], kMaxScratchBlocks * kDgenBlock) != hipSuccess ||
+            hipStreamCreateWithFlags(&sc->st[k], hipStreamNonBlocking) != hipSuccess) {
+            for (int q = 0; q < 2; ++q) {
+                if (sc->buf[q]) (void)hipFree(sc->buf[q]);
+                if (sc->st[q]) (void)hipStreamDestroy(sc->st[q]);
+            }
+            delete sc;
+            return s3dg_internal_fail(S3DG_EHIP, "generator scratch allocation failed");
+        }
+    }
+    g->sc = sc;
     return S3DG_OK;
+}
+
+void release_scratch(s3dg_gen *g) {
+    if (!g->sc) return;
+    for (int k = 0; k < 2; ++k) (void)hipStreamSynchronize(g->sc->st[k]);
+    std::lock_guard<std::mutex> lk(pool_mu);
+    pool.push_back(g->sc);
+    g->sc = nullptr;
 }
 
 // Bytes [pos, pos+n) of the object into host `buf`: covering 1 MiB blocks are
@@ -74,23 +107,24 @@ int ensure_scratch(s3dg_gen *g) {
 // overlaps chunk k's D2H), then exactly the requested bytes are copied out.
 int fill_range(s3dg_gen *g, uint8_t *buf, uint64_t pos, uint64_t n) {
     if (n == 0) return S3DG_OK;
-    if (int r = ensure_scratch(g)) return r;
+    if (int r = acquire_scratch(g)) return r;
+    Scratch *sc = g->sc;
     const uint64_t b0 = pos / kDgenBlock, b1 = (pos + n + kDgenBlock - 1) / kDgenBlock;
     int k = 0;
-    for (uint64_t pb = b0; pb < b1; pb += g->scratch_blocks, ++k) {
-        const uint64_t pe = pb + g->scratch_blocks < b1 ? pb + g->scratch_blocks : b1;
+    for (uint64_t pb = b0; pb < b1; pb += kMaxScratchBlocks, ++k) {
+        const uint64_t pe = pb + kMaxScratchBlocks < b1 ? pb + kMaxScratchBlocks : b1;
         const int sl = k & 1;
-        if (int r = s3dg_dgen_fill(g->ctx, g->scratch[sl], g->size, pb, pe, g->dedup, g->f_num,
-                                   g->f_den, g->seed, g->st[sl]))
+        if (int r = s3dg_dgen_fill(g->ctx, sc->buf[sl], g->size, pb, pe, g->dedup, g->f_num,
+                                   g->f_den, g->seed, sc->st[sl]))
             return r;
         const uint64_t lo = pb * kDgenBlock > pos ? pb * kDgenBlock : pos;
         const uint64_t hi = pe * kDgenBlock < pos + n ? pe * kDgenBlock : pos + n;
-        GEN_HIP(hipMemcpyAsync(buf + (lo - pos), (uint8_t *)g->scratch[sl] + (lo - pb * kDgenBlock),
-                               hi - lo, hipMemcpyDeviceToHost, g->st[sl]),
+        GEN_HIP(hipMemcpyAsync(buf + (lo - pos), (uint8_t *)sc->buf[sl] + (lo - pb * kDgenBlock),
+                               hi - lo, hipMemcpyDeviceToHost, sc->st[sl]),
                 "hipMemcpyAsync(D2H)");
     }
-    GEN_HIP(hipStreamSynchronize(g->st[0]), "hipStreamSynchronize");
-    GEN_HIP(hipStreamSynchronize(g->st[1]), "hipStreamSynchronize");
+    GEN_HIP(hipStreamSynchronize(sc->st[0]), "hipStreamSynchronize");
+    GEN_HIP(hipStreamSynchronize(sc->st[1]), "hipStreamSynchronize");
     return S3DG_OK;
 }
 
@@ -126,10 +160,7 @@ int s3dg_gen_create(uint64_t size, uint64_t dedup, uint64_t compress, int has_se
 
 int s3dg_gen_destroy(s3dg_gen *g) {
     if (!g) return S3DG_OK;
-    for (int k = 0; k < 2; ++k) {
-        if (g->st[k]) { (void)hipStreamSynchronize(g->st[k]); (void)hipStreamDestroy(g->st[k]); }
-        if (g->scratch[k]) (void)hipFree(g->scratch[k]);
-    }
+    release_scratch(g);
     delete g;
     return S3DG_OK;
 }

@@ -7,6 +7,7 @@
 #include "s3dlio_gpu.h"
 
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -134,24 +135,30 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
     if (out_len < L.total) return s3dg_internal_fail(S3DG_EINVAL, "output buffer too small");
     uint32_t crc_x = crc32_host_update(0, L.hx.data(), L.hx.size());
     if (L.x_data) {
-        void *dev = nullptr;
-        hipStream_t s = nullptr;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+        // cached grow-only device buffer + stream (one build at a time)
+        static std::mutex mu;
+        static void *dev = nullptr;
+        static uint64_t cap = 0;
+        static hipStream_t s = nullptr;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
             return s3dg_internal_fail(S3DG_EHIP, "hipStreamCreate");
-        int r = S3DG_OK;
-        uint32_t cd = 0;
-        if (hipMalloc(&dev, L.x_data) != hipSuccess) {
-            r = s3dg_internal_fail(S3DG_ENOMEM, "hipMalloc(npz x-data)");
-        } else if ((r = s3dg_xoshiro_fill(ctx, dev, L.x_data, 2u << 20, 0, s)) == S3DG_OK &&   // :376-383
-                   (r = s3dg_internal_crc_device(ctx, dev, L.x_data, s, &cd)) == S3DG_OK) {
-            crc_x = crc32_combine(crc_x, cd, L.x_data);                                         // :386
-            if (hipMemcpyAsync(out + L.off_x_data, dev, L.x_data, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess)
-                r = s3dg_internal_fail(S3DG_EHIP, "npz x-data D2H");
+        if (L.x_data > cap) {
+            if (dev) (void)hipFree(dev);
+            dev = nullptr;
+            cap = 0;
+            if (hipMalloc(&dev, L.x_data) != hipSuccess)
+                return s3dg_internal_fail(S3DG_ENOMEM, "hipMalloc(npz x-data)");
+            cap = L.x_data;
         }
-        if (dev) (void)hipFree(dev);
-        (void)hipStreamDestroy(s);
-        if (r) return r;
+        uint32_t cd = 0;
+        if (int r = s3dg_xoshiro_fill(ctx, dev, L.x_data, 2u << 20, 0, s)) return r;   // :376-383
+        // D2H, then the CRC kernel (stream order; both only read the keystream)
+        if (hipMemcpyAsync(out + L.off_x_data, dev, L.x_data, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return s3dg_internal_fail(S3DG_EHIP, "npz x-data D2H");
+        if (int r = s3dg_internal_crc_device(ctx, dev, L.x_data, s, &cd)) return r;
+        crc_x = crc32_combine(crc_x, cd, L.x_data);                                    // :386
+        if (hipStreamSynchronize(s) != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, "npz sync");
     }
     // x.npy: local header + NPY header (:368-372, patched :389-392)
     local_header(out, "x.npy", crc_x, (uint32_t)L.x_npy);

@@ -85,11 +85,11 @@ class _Gen:
 
 
 def _new_bytes(size: int, dedup: int, compress, seed: int | None) -> memoryview:
-    out = bytearray(size)
+    out = np.empty(size, np.uint8)           # every byte is written by the generator
     if size:
         g = _Gen(size, dedup, compress, seed)
         try:
-            g.fill(int(np.frombuffer(out, np.uint8).ctypes.data), size)
+            g.fill(int(out.ctypes.data), size)
         finally:
             g.close()
     return memoryview(out).toreadonly()      # BytesView: read-only, zero-copy buffer

@@ -47,10 +47,10 @@ def generate_npz_bytes(shape, dtype: str = "<f4", num_samples: int = 1):
     """Return the NPZ archive as a read-only zero-copy buffer (BytesView)."""
     arr, nd = _shape_arr(shape)
     total = npz_size(shape, dtype, num_samples)
-    out = bytearray(total)
+    out = np.empty(total, np.uint8)          # every byte is written by the builder
     try:
         call("s3dg_npz_build", default_context()._h, arr, nd, dtype.encode(), int(num_samples),
-             int(np.frombuffer(out, np.uint8).ctypes.data), total)
+             int(out.ctypes.data), total)
     except Exception as e:   # the reference maps errors to RuntimeError (:409)
         raise RuntimeError(str(e)) from e
     return memoryview(out).toreadonly()
