@@ -45,6 +45,8 @@ CONFIGS = {
     5: dict(name="cfg5: 100000 x 8 MiB, dedup=2 compress=3 (total over all GPUs)", n=100000,
             size=8 * MiB, dedup=2, compress=3, scaling="strong"),
     # not a BASELINE config: the K2 keystream (npz x-fill, npz.rs:376-383) over the cfg2 footprint
+    7: dict(name="diag: cfg2 objects (10000 x 8 MiB, d1 c1) through the batch API", n=10000,
+            size=None, dedup=1, compress=1, scaling="weak", uniform=8 * MiB),
     6: dict(name="k2: keystream fill, 10000 x 8 MiB as 2 MiB Xoshiro256++ chunks", n=10000,
             size=8 * MiB, dedup=1, compress=1, scaling="weak", keystream=True),
 }
@@ -137,7 +139,7 @@ def main() -> int:
                 slot_obj[s] = (lo + s0 + s, size, s * stride)
         step_bytes = n_rank * size
     else:
-        sizes = log_uniform_sizes(lo + n_rank)[lo:]
+        sizes = ([cfg["uniform"]] * n_rank) if cfg.get("uniform") else log_uniform_sizes(lo + n_rank)[lo:]
         offs, cur, batch_start, batches = [], 0, 0, []
         for j, sz in enumerate(sizes):
             st = (sz + 4095) // 4096 * 4096
@@ -226,6 +228,8 @@ def main() -> int:
             exp = OC.fill_controlled(size, cfg["dedup"], fn, fd, object_entropy(SEED_BASE, j), base)
             ok &= sha(got) == sha(exp)
         verified = bool(cp.max(0.0 if ok else 1.0) == 0.0)
+        if not verified:
+            print("bench: VERIFICATION FAILED: sampled objects differ from the oracle", file=sys.stderr)
 
     # ---- write-only ceiling on the same buffer (same store path) -----------------------
     ceil_bytes = min(int(ring.numel()), 16 * GiB) // 4096 * 4096

@@ -63,8 +63,8 @@ int s3dg_set_base_block(s3dg_ctx *ctx, const uint8_t *base4096);
 /* Base block = Xoshiro256++(seed_from_u64(seed)).fill_bytes(4096). */
 int s3dg_set_base_block_seed(s3dg_ctx *ctx, uint64_t seed);
 int s3dg_get_base_block(s3dg_ctx *ctx, uint8_t *out4096);
-/* Wave64s per 4 KiB block = workgroup size / 64: 1, 2 (default) or 4
- * (0 = default).  A tuning knob; results are identical for every value. */
+/* Wave64s per 4 KiB block = workgroup size / 64: 1, 2 or 4; 0 = auto
+ * (2 for streams, 1 for batches).  A tuning knob; results are identical. */
 int s3dg_set_waves_per_block(s3dg_ctx *ctx, int waves);
 /* 1 = nontemporal stores, 0 = plain stores (default). */
 int s3dg_set_nontemporal(s3dg_ctx *ctx, int on);

@@ -31,14 +31,14 @@ using namespace s3dg;
 struct s3dg_ctx {
     int device = 0;
     bool nontemporal = false;          // plain stores measured faster
-    int waves_per_block = 2;           // measured best on MI355X
+    int waves_per_block = 0;           // 0 = auto: 2 for streams, 1 for batches (measured)
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // batch descriptor table (device) + pinned staging, grown on demand
     ObjEntry *tab_dev = nullptr;
     ObjEntry *tab_host = nullptr;
     uint64_t tab_cap = 0;
-    uint32_t *tile_obj = nullptr;      // tile -> object entry map (device)
+    TileRec *tile_obj = nullptr;       // per-tile records (device)
     uint64_t tile_cap = 0;
     hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
     std::map<uint64_t, uint64_t *> jtabs;   // (lpc << 32 | span) -> device jump table
@@ -113,10 +113,10 @@ int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den
     return S3DG_OK;
 }
 
-LaunchCfg cfg_for(s3dg_ctx *c) {
+LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false) {
     LaunchCfg lc;
     lc.nontemporal = c->nontemporal;
-    lc.waves_per_block = c->waves_per_block;
+    lc.waves_per_block = c->waves_per_block ? c->waves_per_block : (batch ? 1 : 2);
     return lc;
 }
 
@@ -213,8 +213,7 @@ int s3dg_get_base_block(s3dg_ctx *c, uint8_t *out) {
 
 int s3dg_set_waves_per_block(s3dg_ctx *c, int waves) {
     if (!c) return fail(S3DG_EINVAL, "null context");
-    if (waves == 0) waves = 2;
-    if (waves != 1 && waves != 2 && waves != 4) return fail(S3DG_EINVAL, "waves per block must be 1, 2 or 4");
+    if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(S3DG_EINVAL, "waves per block must be 1, 2 or 4");
     c->waves_per_block = waves;
     return S3DG_OK;
 }
@@ -311,14 +310,14 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     if (c->crc_seg) (void)hipFree(c->crc_seg);
         c->tile_obj = nullptr; c->tile_cap = 0;
         const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
-        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(uint32_t)), "hipMalloc(tile map)");
+        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");
         c->tile_cap = cap;
     }
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemcpyAsync(c->tab_dev, c->tab_host, m * sizeof(ObjEntry), hipMemcpyHostToDevice, s),
             "hipMemcpyAsync(batch table)");
     HIP_TRY(hipEventRecord(c->tab_free, s), "hipEventRecord");
-    HIP_TRY(launch_fill_batch(cfg_for(c), (uint8_t *)dst_base, c->tab_dev, m, tiles,
+    HIP_TRY(launch_fill_batch(cfg_for(c, true), (uint8_t *)dst_base, c->tab_dev, m, tiles,
                               c->tile_obj, c->base_dev, s),
             "launch k_fill_batch");
     return S3DG_OK;

@@ -175,6 +175,7 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
             *seg_cap = nreg;
         }
         const uint64_t wgs = (nreg + 3) / 4;
+        (void)hipGetLastError();
         hipLaunchKernelGGL(k_crc32_regions, dim3((uint32_t)wgs), dim3(256), 0, s, dev, nreg, rows,
                            (const CrcTables *)*tab_cache,
                            (const uint32_t *)((uint8_t *)*tab_cache + sizeof(CrcTables)), *seg_cache);

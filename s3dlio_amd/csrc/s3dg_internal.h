@@ -37,6 +37,18 @@ struct ObjEntry {
     PrefixParams pp;
 };
 
+// One 64-block tile of a batch object, written by k_tile_map so the fill
+// kernel reaches everything with a single 64-byte scalar load.
+struct TileRec {
+    uint64_t dst_off;      // byte offset of the tile's first block
+    uint64_t size;         // object size
+    uint64_t entropy;
+    uint32_t first;        // first block index of the tile within the object
+    uint32_t pad;
+    PrefixParams pp;
+};
+static_assert(sizeof(TileRec) == 64, "TileRec is one s_load_dwordx16");
+
 struct LaunchCfg {
     bool nontemporal;
     int waves_per_block;   // 1, 2 or 4 wave64s per 4 KiB block (one workgroup)
@@ -48,7 +60,7 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               PrefixParams pp, const void *base_dev, hipStream_t s);
 
 hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, uint32_t *tile_obj,
+                             uint64_t n, uint64_t total_tiles, TileRec *tiles,
                              const void *base_dev, hipStream_t s);
 
 // K2 keystream launch: chunks [chunk0, chunk0 + nchunks) of an obj_len-byte

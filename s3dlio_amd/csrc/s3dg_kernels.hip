@@ -247,32 +247,39 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t 
                   seed_base + ((first_obj + j) << 32), pp, base);
 }
 
-// Batch: workgroup g -> tile g/64 -> object tab[tile_obj[g/64]], block
-// (g%64) + 64*(tile - tile_begin).  Tiles past an object's end exit.
+// Batch: workgroup g -> tile record g/64 (one scalar load), block
+// first + (g % 64) of that object; blocks past the object's end exit.
 template <bool NT, int NW>
-__global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const ObjEntry *tab,
-                                                    const uint32_t *tile_obj, uint64_t g0,
-                                                    const u32x4 *base) {
+__global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
+                                                        uint64_t g0, const u32x4 *base) {
     __shared__ __attribute__((aligned(16))) BlockLds S;
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t g = g0 + blockIdx.x;
-    const uint64_t tile = g >> 6;
-    const ObjEntry e = tab[tile_obj[tile]];
-    const uint64_t ib = (tile - e.tile_begin) * kTileBlocks + (g & 63);
+    const TileRec e = tiles[g >> 6];
+    const uint32_t k = (uint32_t)(g & 63);
+    const uint64_t ib = (uint64_t)e.first + k;
     if (ib * kBlk >= e.size) return;               // uniform for the whole workgroup
-    gen_block<NT, NW>(dst_base + e.dst_off + ib * kBlk, S, t, wave, (uint32_t)ib, e.size, e.entropy,
-                  e.pp, base);
+    gen_block<NT, NW>(dst_base + e.dst_off + (uint64_t)k * kBlk, S, t, wave, (uint32_t)ib, e.size,
+                      e.entropy, e.pp, base);
 }
 
-// tile_obj[tile] = object entry index, for every tile of every object.
-__global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t n,
-                                                  uint32_t *tile_obj) {
+// tiles[tile] = record of every 64-block tile of every object.
+__global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t n, TileRec *tiles) {
     const uint64_t k = blockIdx.x;
     if (k >= n) return;
     const ObjEntry e = tab[k];
     const uint64_t nt = ((e.size + kBlk - 1) / kBlk + kTileBlocks - 1) / kTileBlocks;
-    for (uint64_t q = threadIdx.x; q < nt; q += blockDim.x) tile_obj[e.tile_begin + q] = (uint32_t)k;
+    for (uint64_t q = threadIdx.x; q < nt; q += blockDim.x) {
+        TileRec r;
+        r.dst_off = e.dst_off + q * kTileBlocks * kBlk;
+        r.size = e.size;
+        r.entropy = e.entropy;
+        r.first = (uint32_t)(q * kTileBlocks);
+        r.pad = 0;
+        r.pp = e.pp;
+        tiles[e.tile_begin + q] = r;
+    }
 }
 
 // Write-only ceiling in the same shape (one 4 KiB chunk per 256-thread workgroup).
@@ -397,7 +404,9 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
     }
 }
 
-constexpr uint64_t kMaxGridX = 1ull << 30;
+// Grid sizes are 32-bit WORK-ITEM counts in the AQL dispatch packet: cap a
+// launch at 2^22 workgroups per dimension (x 256 threads < 2^32).
+constexpr uint64_t kMaxGridX = 1ull << 22;
 
 template <bool NT, int NW>
 void launch_stream_one(dim3 g, hipStream_t s, uint8_t *d, uint64_t obj_size, uint64_t stride,
@@ -408,9 +417,9 @@ void launch_stream_one(dim3 g, hipStream_t s, uint8_t *d, uint64_t obj_size, uin
 }
 
 template <bool NT, int NW>
-void launch_batch_one(dim3 g, hipStream_t s, uint8_t *d, const ObjEntry *tab,
-                      const uint32_t *tile_obj, uint64_t g0, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), 0, s, d, tab, tile_obj, g0, b);
+void launch_batch_one(dim3 g, hipStream_t s, uint8_t *d, const TileRec *tiles, uint64_t g0,
+                      const u32x4 *b) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), 0, s, d, tiles, g0, b);
 }
 
 #define S3DG_DISPATCH(fn, lc, ...)                                              \
@@ -432,6 +441,7 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               uint64_t stride, uint64_t n_objs, uint32_t blk_lo,
                               uint32_t blk_hi, uint64_t seed_base, uint64_t first_obj,
                               PrefixParams pp, const void *base_dev, hipStream_t s) {
+    (void)hipGetLastError();   // drop stale errors of unrelated calls (e.g. torch pointer probes)
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
     const uint32_t nx = blk_hi - blk_lo;
     for (uint64_t y0 = 0; y0 < n_objs; y0 += 65535) {
@@ -448,16 +458,17 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
 }
 
 hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, uint32_t *tile_obj,
+                             uint64_t n, uint64_t total_tiles, TileRec *tiles,
                              const void *base_dev, hipStream_t s) {
-    hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tile_obj);
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tiles);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
     const uint64_t total = total_tiles * kTileBlocks;
     for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
-        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), s, dst_base, tab, tile_obj, g0, b);
+        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), s, dst_base, tiles, g0, b);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -466,6 +477,7 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
 
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
                            hipStream_t s) {
+    (void)hipGetLastError();
     const uint64_t cpw = 64 / A.lpc;
     const uint64_t waves = (A.nchunks + cpw - 1) / cpw;
     const uint64_t wgs = (waves + 3) / 4;
@@ -476,6 +488,7 @@ hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len, uint32_t pattern,
                                 hipStream_t s) {
+    (void)hipGetLastError();
     const uint64_t nch = len / kBlk;
     for (uint64_t g0 = 0; g0 < nch; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((nch - g0) < kMaxGridX ? (nch - g0) : kMaxGridX);

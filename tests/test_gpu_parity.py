@@ -103,7 +103,9 @@ def test_stream_vs_oracle(gpu_ctx, torch, oracle, base, size, stride, n, d, c, f
     assert (got[stride * n:] == GUARD).all()
 
 
-def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base):
+@pytest.mark.parametrize("waves", [1, 2, 4])
+def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves):
+    gpu_ctx.set_waves_per_block(waves)
     rnd = random.Random(7)
     sizes = [0, 1, 5, 31, 32, 33, 4095, 4096, 4097, 2**20 + 3, 3 * 2**20, 65536 * 64 + 11]
     sizes += [int(np.exp(rnd.uniform(np.log(4096), np.log(4 * 2**20)))) for _ in range(40)]
@@ -121,8 +123,9 @@ def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base):
     for (o, sz, e, d, c), end in zip(objs, nxt):
         fn, fd = P.compress_ratio(c)
         exp = oracle.fill_controlled(sz, d, fn, fd, e, base)
-        assert np.array_equal(got[o:o + sz], exp), (o, sz, d, c)
+        assert np.array_equal(got[o:o + sz], exp), (waves, o, sz, d, c)
         assert (got[o + sz:end] == GUARD).all()
+    gpu_ctx.set_waves_per_block(0)
 
 
 def test_range_pieces_compose(gpu_ctx, torch, oracle, base):
@@ -268,3 +271,29 @@ def test_keystream_full_size_properties(gpu_ctx, torch, oracle):
         assert np.array_equal(t[k * 2**21:(k + 1) * 2**21].cpu().numpy(), exp), k
     hist = torch.bincount(t[:2**30].to(torch.int32), minlength=256).double()
     assert float((hist.max() - hist.min()) / hist.mean()) < 0.01
+
+
+def test_launch_splitting_large_grids(gpu_ctx, torch, oracle, base):
+    """Launches are split at 2^22 workgroups per grid dimension (AQL grid
+    sizes are 32-bit work-item counts).  One 17 GiB object (stream path) and a
+    17.5 GiB batch both cross that split; both checked against the oracle."""
+    size = 17 * 2**30 + 4096 * 3 + 5
+    t = torch.empty(size, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_controlled(t, size, dedup=1, compress=3, entropy=123)
+    torch.cuda.synchronize()
+    exp = oracle.fill_controlled(size, 1, 2, 3, 123, base)
+    for lo, hi in [(0, 2**24), (2**34 - 2**20, 2**34 + 2**20), (size - 2**24, size)]:
+        assert np.array_equal(t[lo:hi].cpu().numpy(), exp[lo:hi]), (lo, hi)
+    del t, exp
+    for waves in (1, 2, 4):
+        gpu_ctx.set_waves_per_block(waves)
+        osz = 5 * 2**29 + 100                                  # 2.5 GiB + 100 B
+        stride = (osz + 4095) // 4096 * 4096
+        objs = [(k * stride, osz, P.object_entropy(SEED_BASE, k), 2, 2) for k in range(7)]
+        out = torch.empty(7 * stride, dtype=torch.uint8, device="cuda")
+        gpu_ctx.fill_batch(out, objs)
+        torch.cuda.synchronize()
+        exp = oracle.fill_controlled(osz, 2, 1, 2, P.object_entropy(SEED_BASE, 6), base)
+        assert np.array_equal(out[6 * stride:6 * stride + osz].cpu().numpy(), exp), waves
+        del out, exp
+    gpu_ctx.set_waves_per_block(0)
