@@ -86,6 +86,11 @@ int s3dg_fill_controlled_range(s3dg_ctx *ctx, void *dst, uint64_t len,
                                uint64_t blk_lo, uint64_t blk_hi, uint64_t dedup,
                                uint32_t f_num, uint32_t f_den, uint64_t entropy,
                                void *stream);
+/* Seeded analogue of generate_random_data (src/data_gen.rs:102-132, whose
+ * ThreadRng makes it unseedable): the context's base block tiled per 4 KiB
+ * block, bytes [0, min(32, L)) then [L-32, L) when L > 2048 overwritten by
+ * SmallRng::seed_from_u64(entropy + i).fill_bytes for block i. */
+int s3dg_random_data(s3dg_ctx *ctx, void *dst, uint64_t len, uint64_t entropy, void *stream);
 /* n equal-size objects, object j at dst + j*stride, entropy
  * s3dg_object_entropy(seed_base, first_obj + j). */
 int s3dg_fill_controlled_stream(s3dg_ctx *ctx, void *dst, uint64_t obj_size,
@@ -169,7 +174,34 @@ int s3dg_gen_reset(s3dg_gen *gen);
 int s3dg_generate_data(uint8_t *buf, uint64_t size, uint64_t dedup, uint64_t compress,
                        int has_seed, uint64_t seed);
 
+/* ---- object assembly: generate_object (src/data_gen.rs:29-94) ------------ */
+enum { S3DG_OBJ_NPZ = 0, S3DG_OBJ_TFRECORD = 1, S3DG_OBJ_HDF5 = 2, S3DG_OBJ_RAW = 3 };
+enum { S3DG_MODE_STREAMING = 0, S3DG_MODE_SINGLE_PASS = 1 };
+/* Bytes generate_object produces for (type, elements, element_size). */
+int s3dg_object_size(int type, uint64_t elements, uint64_t element_size, uint64_t *out);
+/* generate_object(&Config) into `out` (>= s3dg_object_size bytes):
+ * use_controlled=0 -> generate_random_data payload, else the dgen-contract
+ * payload; then build_raw / build_tfrecord / build_npz.  HDF5 -> S3DG_EINVAL
+ * (as a reference build without the hdf5 feature).  has_seed=0 reproduces
+ * the reference's non-deterministic entropy. */
+int s3dg_generate_object(int type, uint64_t elements, uint64_t element_size, int use_controlled,
+                         uint64_t dedup, uint64_t compress, int mode, int has_seed, uint64_t seed,
+                         uint8_t *out, uint64_t out_len, uint64_t *written);
+/* build_tfrecord_with_index (src/data_formats/tfrecord.rs:47-75): records of
+ * record_size bytes from `data` -> out (records * (16 + record_size) bytes;
+ * may alias data shifted by 12 for one record); index_out (nullable) gets
+ * 16 bytes <offset u64, length u64> per record. */
+int s3dg_build_tfrecord(uint64_t records, uint64_t record_size, const uint8_t *data, uint8_t *out,
+                        uint8_t *index_out);
+/* build_npz (src/data_formats/npz.rs:114-132): "data.npy" in a stored ZIP. */
+int s3dg_npz_legacy_size(uint64_t elements, uint64_t data_len, uint64_t *out);
+int s3dg_build_npz(uint64_t elements, const uint8_t *data, uint64_t data_len, uint8_t *out,
+                   uint64_t out_len);
+
 /* ---- host-buffer drop-ins (src/data_gen.rs:151 signature) ---------------- */
+/* generate_random_data(size) (src/data_gen.rs:102): seeded analogue layout
+ * with time entropy and a per-process random BASE_BLOCK. */
+int s3dlio_generate_random_data(uint8_t *buf, size_t size);
 /* fill_controlled_data(buf, dedup, compress): time-based entropy and a
  * per-process random base block, exactly as the reference; generated on the
  * GPU of the process-default context (env S3DLIO_GPU_DEVICE, default 0) and

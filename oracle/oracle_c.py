@@ -56,6 +56,7 @@ def lib():
         L.s3dgo_fill_stream_mt.restype = ctypes.c_int
         L.s3dgo_xoshiro_chunks.argtypes = [u8p, u64, u64, u64]
         L.s3dgo_dgen_fill.argtypes = [u8p, u64, u64, u64, u64, u64]
+        L.s3dgo_random_data.argtypes = [u8p, u64, u64, u8p]
         _lib = L
     return _lib
 
@@ -128,4 +129,11 @@ def xoshiro_chunks(length: int, chunk: int, seed_base: int) -> np.ndarray:
 def dgen_fill(size: int, dedup: int, f_num: int, f_den: int, seed: int) -> np.ndarray:
     out = np.empty(size, np.uint8)
     lib().s3dgo_dgen_fill(_ptr(out), size, dedup, f_num, f_den, seed & (2**64 - 1))
+    return out
+
+
+def random_data(size: int, entropy: int, base: np.ndarray) -> np.ndarray:
+    out = np.empty(size, np.uint8)
+    base = np.ascontiguousarray(base, np.uint8)
+    lib().s3dgo_random_data(_ptr(out), size, entropy & (2**64 - 1), _ptr(base))
     return out

@@ -159,3 +159,20 @@ def dgen_fill(size: int, dedup: int, f_num: int, f_den: int, seed: int) -> bytes
         blk[:z] = bytes(z)
         out += blk
     return bytes(out)
+
+
+def random_data(size: int, entropy: int, base: bytes) -> bytes:
+    """Seeded analogue of generate_random_data (src/data_gen.rs:102-132), per-block seeds."""
+    out = bytearray()
+    i = 0
+    while len(out) < size:
+        bs = min(BLK, size - len(out))
+        blk = bytearray(base[:bs])
+        rng = Xoshiro256pp.seed_from_u64((entropy + i) & M64)
+        m = min(bs, MOD)
+        blk[:m] = rng.fill_bytes(m)
+        if bs > HALF:
+            blk[bs - MOD:] = rng.fill_bytes(MOD)
+        out += blk
+        i += 1
+    return bytes(out)

@@ -260,3 +260,21 @@ void s3dgo_dgen_fill(uint8_t *buf, uint64_t size, uint64_t dedup, uint64_t f_num
         memset(buf + off, 0, (L * f_num) / f_den);
     }
 }
+
+/* ---- seeded analogue of generate_random_data (src/data_gen.rs:102-132) ---- */
+/* Reference: BASE_BLOCK tiled per 4 KiB block (:104-107), then one
+ * sequential ThreadRng fills [0, min(32, bs)) (:115-122) and, when
+ * bs > HALF_BLK, [bs-32, bs) (:124-126) of every block.  ThreadRng is
+ * unseedable, so the build seeds each block separately: block i uses
+ * SmallRng::seed_from_u64(entropy + i) for both fills (parity impossible,
+ * structure identical). */
+void s3dgo_random_data(uint8_t *buf, uint64_t size, uint64_t entropy, const uint8_t *base) {
+    for (uint64_t off = 0, i = 0; off < size; off += S3DGO_BLK, ++i) {
+        uint64_t bs = size - off < S3DGO_BLK ? size - off : S3DGO_BLK;
+        memcpy(buf + off, base, bs);
+        uint64_t s[4];
+        s3dgo_xoshiro_seed(s, entropy + i);
+        s3dgo_fill_bytes(s, buf + off, bs < S3DGO_MOD ? bs : S3DGO_MOD);
+        if (bs > S3DGO_HALF) s3dgo_fill_bytes(s, buf + off + bs - S3DGO_MOD, S3DGO_MOD);
+    }
+}

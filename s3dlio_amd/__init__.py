@@ -17,4 +17,8 @@ from .datagen import (DataGenerator, Generator, ObjectGen, default_data_gen_thre
 
 from .npz import crc32_combine, crc32_device, generate_npz_bytes, npz_size  # noqa: F401
 
+from .objects import (Config, DataGenMode, ObjectType, build_npz, build_raw,  # noqa: F401
+                      build_tfrecord, build_tfrecord_with_index, generate_object,
+                      generate_random_data, object_size)
+
 __version__ = "0.1.0"

@@ -51,6 +51,7 @@ SIGNATURES = {
     "s3dg_unique_blocks": (c_u64, [c_u64, c_u64]),
     "s3dg_compress_ratio": (c_int, [c_u64, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]),
     "s3dg_object_entropy": (c_u64, [c_u64, c_u64]),
+    "s3dg_random_data": (c_int, [c_vp, c_vp, c_u64, c_u64, c_vp]),
     "s3dg_fill_controlled": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),
     "s3dg_fill_controlled_range": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32,
                                            c_u64, c_vp]),
@@ -94,6 +95,13 @@ SIGNATURES = {
                                             ctypes.c_size_t]),
     "s3dlio_fill_controlled_data_seeded": (c_int, [c_vp, ctypes.c_size_t, ctypes.c_size_t,
                                                    ctypes.c_size_t, c_u64, c_u8p]),
+    "s3dg_object_size": (c_int, [c_int, c_u64, c_u64, ctypes.POINTER(c_u64)]),
+    "s3dg_generate_object": (c_int, [c_int, c_u64, c_u64, c_int, c_u64, c_u64, c_int, c_int, c_u64,
+                                     c_vp, c_u64, ctypes.POINTER(c_u64)]),
+    "s3dg_build_tfrecord": (c_int, [c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "s3dg_npz_legacy_size": (c_int, [c_u64, c_u64, ctypes.POINTER(c_u64)]),
+    "s3dg_build_npz": (c_int, [c_u64, c_vp, c_u64, c_vp, c_u64]),
+    "s3dlio_generate_random_data": (c_int, [c_vp, ctypes.c_size_t]),
     "s3dg_last_error": (ctypes.c_char_p, []),
     "s3dg_version": (ctypes.c_char_p, []),
 }

@@ -242,6 +242,23 @@ int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t bl
     return S3DG_OK;
 }
 
+int s3dg_random_data(s3dg_ctx *c, void *dst, uint64_t len, uint64_t entropy, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (len == 0) return S3DG_OK;
+    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    const uint64_t nb = (len + kBlk - 1) / kBlk;
+    if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    PrefixParams pp{};
+    pp.unique = 0xFFFFFFFFu;            // block i seeded entropy + i
+    pp.f_den = 0;                       // random-data layout
+    pp.m_unique = fastmod_magic(1);
+    pp.m_fden = fastmod_magic(1);
+    HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, len, 0, 1, 0, (uint32_t)nb, entropy, 0,
+                               pp, c->base_dev, (hipStream_t)stream),
+            "launch k_fill_stream(random data)");
+    return S3DG_OK;
+}
+
 int s3dg_fill_controlled(s3dg_ctx *c, void *dst, uint64_t len, uint64_t dedup, uint32_t f_num,
                          uint32_t f_den, uint64_t entropy, void *stream) {
     return s3dg_fill_controlled_range(c, dst, len, 0, ~0ull, dedup, f_num, f_den, entropy, stream);
@@ -513,6 +530,8 @@ struct DefaultCtx {
     s3dg_ctx *ctx = nullptr;
     uint8_t proc_base[kBlk];           // A_BASE_BLOCK equivalent (random, once per process)
     bool have_proc_base = false;
+    uint8_t proc_base2[kBlk];          // BASE_BLOCK equivalent (src/constants.rs:725-729)
+    bool have_proc_base2 = false;
     void *scratch[2] = {nullptr, nullptr};
     hipStream_t st[2] = {nullptr, nullptr};
     static constexpr uint64_t kChunk = 64ull << 20;   // 64 MiB per device chunk
@@ -559,6 +578,43 @@ int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t dedup, uint64_
     return S3DG_OK;
 }
 
+// generate_random_data layout (seeded analogue) into a host buffer, chunked
+// like fill_host; block i seeded entropy + i.
+int fill_host_random(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t entropy) {
+    const uint64_t nb = (len + kBlk - 1) / kBlk;
+    if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    PrefixParams pp{};
+    pp.unique = 0xFFFFFFFFu;
+    pp.f_den = 0;
+    pp.m_unique = fastmod_magic(1);
+    pp.m_fden = fastmod_magic(1);
+    const uint64_t cb = DefaultCtx::kChunk / kBlk;
+    for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
+        const uint64_t b1 = b0 + cb < nb ? b0 + cb : nb;
+        const int sl = (int)(k & 1);
+        HIP_TRY(launch_fill_stream(cfg_for(D.ctx), (uint8_t *)D.scratch[sl], len, 0, 1, (uint32_t)b0,
+                                   (uint32_t)b1, entropy, 0, pp, D.ctx->base_dev, D.st[sl]),
+                "launch k_fill_stream(random data)");
+        const uint64_t off = b0 * kBlk;
+        const uint64_t n = (b1 * kBlk < len ? b1 * kBlk : len) - off;
+        HIP_TRY(hipMemcpyAsync(buf + off, D.scratch[sl], n, hipMemcpyDeviceToHost, D.st[sl]),
+                "hipMemcpyAsync(D2H)");
+    }
+    HIP_TRY(hipStreamSynchronize(D.st[0]), "hipStreamSynchronize");
+    HIP_TRY(hipStreamSynchronize(D.st[1]), "hipStreamSynchronize");
+    return S3DG_OK;
+}
+
+int random_bytes(uint8_t *dst, size_t n) {
+    size_t got = 0;
+    while (got < n) {
+        ssize_t k = getrandom(dst + got, n - got, 0);
+        if (k <= 0) return fail(S3DG_EINVAL, "getrandom failed");
+        got += (size_t)k;
+    }
+    return S3DG_OK;
+}
+
 uint64_t time_entropy() {      // SystemTime::now() ... as_nanos() as u64, :192-195
     timespec ts;
     clock_gettime(CLOCK_REALTIME, &ts);
@@ -579,6 +635,32 @@ s3dg_ctx *s3dg_internal_default_ctx(int *err) {
     return r ? nullptr : D.ctx;
 }
 
+// generate_random_data payload for generate_object: seeded (ctx default base
+// block, entropy = seed) or unseeded (time entropy + per-process BASE_BLOCK).
+int s3dg_internal_random_host(uint8_t *buf, uint64_t len, uint64_t entropy, int use_process_base) {
+    if (len == 0) return S3DG_OK;
+    DefaultCtx &D = dflt();
+    std::lock_guard<std::mutex> g(D.mu);
+    if (int r = dflt_init(D)) return r;
+    if (!use_process_base) return fill_host_random(D, buf, len, entropy);
+    if (!D.have_proc_base2) {
+        if (int r = random_bytes(D.proc_base2, kBlk)) return r;
+        D.have_proc_base2 = true;
+    }
+    uint8_t saved[kBlk];
+    std::memcpy(saved, D.ctx->base_host, kBlk);
+    if (int r = s3dg_set_base_block(D.ctx, D.proc_base2)) return r;
+    int r = fill_host_random(D, buf, len, time_entropy());
+    int r2 = s3dg_set_base_block(D.ctx, saved);
+    return r ? r : r2;
+}
+
+int s3dlio_generate_random_data(uint8_t *buf, size_t size) {
+    if (size == 0) return S3DG_OK;
+    if (!buf) return fail(S3DG_EINVAL, "null buffer");
+    return s3dg_internal_random_host(buf, size, 0, 1);
+}
+
 int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress) {
     if (len == 0) return S3DG_OK;
     if (!buf) return fail(S3DG_EINVAL, "null buffer");
@@ -586,12 +668,7 @@ int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t c
     std::lock_guard<std::mutex> g(D.mu);
     if (int r = dflt_init(D)) return r;
     if (!D.have_proc_base) {
-        size_t got = 0;
-        while (got < kBlk) {
-            ssize_t k = getrandom(D.proc_base + got, kBlk - got, 0);
-            if (k <= 0) return fail(S3DG_EINVAL, "getrandom failed");
-            got += (size_t)k;
-        }
+        if (int r = random_bytes(D.proc_base, kBlk)) return r;
         D.have_proc_base = true;
     }
     uint8_t saved[kBlk];

@@ -133,9 +133,23 @@ void init_tables() {
 }  // namespace
 
 uint32_t crc32_host_update(uint32_t crc, const uint8_t *p, uint64_t n) {
-    init_tables();
+    {
+        static std::mutex m;
+        std::lock_guard<std::mutex> g(m);
+        init_tables();
+    }
     uint32_t c = ~crc;
-    for (uint64_t i = 0; i < n; ++i) c = (c >> 8) ^ crc_tables[0][(c ^ p[i]) & 0xFF];
+    uint64_t i = 0;
+    for (; i + 8 <= n; i += 8) {                      // slicing-by-8 (little-endian host)
+        uint32_t a, b;
+        memcpy(&a, p + i, 4);
+        memcpy(&b, p + i + 4, 4);
+        a ^= c;
+        c = crc_tables[7][a & 0xFF] ^ crc_tables[6][(a >> 8) & 0xFF] ^ crc_tables[5][(a >> 16) & 0xFF] ^
+            crc_tables[4][a >> 24] ^ crc_tables[3][b & 0xFF] ^ crc_tables[2][(b >> 8) & 0xFF] ^
+            crc_tables[1][(b >> 16) & 0xFF] ^ crc_tables[0][b >> 24];
+    }
+    for (; i < n; ++i) c = (c >> 8) ^ crc_tables[0][(c ^ p[i]) & 0xFF];
     return ~c;
 }
 

@@ -19,7 +19,7 @@ struct PrefixParams {
     uint32_t unique;     // U, src/data_gen.rs:162-167 (0xFFFFFFFF: U == nblocks, u = i)
     uint32_t floor_len;
     uint32_t rem;
-    uint32_t f_den;
+    uint32_t f_den;      // 0: generate_random_data block layout (src/data_gen.rs:102-132)
     uint64_t m_unique;   // Lemire fastmod constants: floor(2^64 / d) + 1
     uint64_t m_fden;
 };

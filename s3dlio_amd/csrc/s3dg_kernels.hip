@@ -110,18 +110,27 @@ __device__ __forceinline__ void plan_block(Plan &P, uint32_t lane, uint32_t i, u
     const uint32_t u = pp.unique == 0xFFFFFFFFu ? i : fastmod(i, pp.m_unique, pp.unique);  // :201
     const uint64_t off = (uint64_t)i * kBlk;
     const uint32_t L = (uint32_t)((size - off) < kBlk ? (size - off) : kBlk);
-    uint32_t cl = pp.floor_len;
-    if (pp.rem) {                     // closed form of :177-190; period f_den in u
-        const uint32_t up = fastmod(u, pp.m_fden, pp.f_den);
-        const uint32_t r0 = pp.f_den <= 65536u ? fastmod(up * pp.rem, pp.m_fden, pp.f_den)
-                                               : (uint32_t)(((uint64_t)up * pp.rem) % pp.f_den);
-        cl += (uint32_t)((uint64_t)r0 + pp.rem >= pp.f_den);
-    }
     P.L = L;
-    P.c = cl < L ? cl : L;                                               // :209
-    P.m = (L - P.c) < kMod ? (L - P.c) : kMod;                           // :212-214
-    P.so = P.c > kHalf ? P.c : kHalf;                                    // :218
-    P.w2 = P.m > 0 && P.so + P.m <= L;                                   // :219
+    if (pp.f_den == 0) {
+        // generate_random_data layout (src/data_gen.rs:102-132): no zero prefix,
+        // first min(32, L) bytes, then the last 32 bytes when L > HALF_BLK
+        P.c = 0;
+        P.m = L < kMod ? L : kMod;
+        P.so = L - kMod;
+        P.w2 = L > kHalf;
+    } else {
+        uint32_t cl = pp.floor_len;
+        if (pp.rem) {                     // closed form of :177-190; period f_den in u
+            const uint32_t up = fastmod(u, pp.m_fden, pp.f_den);
+            const uint32_t r0 = pp.f_den <= 65536u ? fastmod(up * pp.rem, pp.m_fden, pp.f_den)
+                                                   : (uint32_t)(((uint64_t)up * pp.rem) % pp.f_den);
+            cl += (uint32_t)((uint64_t)r0 + pp.rem >= pp.f_den);
+        }
+        P.c = cl < L ? cl : L;                                           // :209
+        P.m = (L - P.c) < kMod ? (L - P.c) : kMod;                       // :212-214
+        P.so = P.c > kHalf ? P.c : kHalf;                                // :218
+        P.w2 = P.m > 0 && P.so + P.m <= L;                               // :219
+    }
 
     // SmallRng::seed_from_u64(u + entropy) (:202-203): state word k =
     // mix64(seed + (k+1)*phi) — lanes 0..3 compute one word each.

@@ -149,6 +149,13 @@ class Context:
         call("s3dg_fill_controlled", self._h, _ptr(dst), int(n), int(dedup), fn, fd,
              int(entropy) & (2**64 - 1), _stream(stream))
 
+    def random_data(self, dst, nbytes: int | None = None, entropy: int = 0, stream=None) -> None:
+        """generate_random_data's layout (src/data_gen.rs:102-132): no zero
+        prefix, one window at 0 and one at L-32 (L > 2048), seeded by `entropy`."""
+        n = _nbytes(dst) if nbytes is None else nbytes
+        call("s3dg_random_data", self._h, _ptr(dst), int(n), int(entropy) & (2**64 - 1),
+             _stream(stream))
+
     def fill_range(self, dst, length: int, blk_lo: int, blk_hi: int, dedup: int = 1,
                    compress=1, entropy: int = 0, stream=None) -> None:
         fn, fd = compress_ratio(compress)
