@@ -171,8 +171,15 @@ def test_gpu_random_data_vs_oracle(S, oracle, golden_base, gpu_ctx, n):
 @pytest.mark.gpu
 def test_gpu_generate_random_data_unseeded(S, gpu_ctx):
     """Unseeded: time entropy + per-process random base block; sizes exact,
-    successive calls differ, bytes incompressible (data_gen.rs:102-132)."""
-    a, b = S.generate_random_data(3 * 2**20 + 5), S.generate_random_data(3 * 2**20 + 5)
-    assert len(a) == len(b) == 3 * 2**20 + 5 and a != b
-    assert len(zlib.compress(a, 1)) > 0.99 * len(a)
+    successive calls differ.  Like the reference (data_gen.rs:102-132), every
+    block is the same base block outside its two 32-B windows, so the output
+    is highly compressible -- that is the reference's behaviour."""
+    n = 3 * 2**20 + 5
+    a, b = S.generate_random_data(n), S.generate_random_data(n)
+    assert len(a) == len(b) == n and a != b
+    blocks = np.frombuffer(a[:n - n % 4096], np.uint8).reshape(-1, 4096)
+    assert (blocks[:, 32:4064] == blocks[0, 32:4064]).all()
+    assert len({bytes(r[:32]) for r in blocks}) == len(blocks)
+    assert len({bytes(r[-32:]) for r in blocks}) == len(blocks)
+    assert len(zlib.compress(a, 1)) < 0.1 * n
     assert S.generate_random_data(0) == b""
