@@ -38,6 +38,7 @@ enum {
     S3DG_EINVAL = -1,   /* bad argument (null, misaligned, out of range) */
     S3DG_EHIP = -2,     /* HIP runtime error (message in s3dg_last_error) */
     S3DG_ENOMEM = -3,
+    S3DG_EIO = -4,      /* file-system error in the put pipeline */
 };
 
 typedef struct s3dg_ctx s3dg_ctx;
@@ -197,6 +198,34 @@ int s3dg_build_tfrecord(uint64_t records, uint64_t record_size, const uint8_t *d
 int s3dg_npz_legacy_size(uint64_t elements, uint64_t data_len, uint64_t *out);
 int s3dg_build_npz(uint64_t elements, const uint8_t *data, uint64_t data_len, uint8_t *out,
                    uint64_t out_len);
+
+/* ---- put pipeline: per-object payloads -> files -------- */
+/* Replaces put_objects_with_random_data_and_type (src/s3_utils.rs:1717-1750)
+ * + put_objects_parallel_with_progress (:1812-1868) + FileSystemObjectStore::put
+ * (src/file_store.rs:550-569) for file:// targets, with one payload PER OBJECT
+ * (the reference PUTs one buffer to every URI).  Object j (paths[j], a plain
+ * file-system path: the file:// prefix already stripped) is framed as
+ * object_type with elements = 1, element_size = size (python_core_api.rs:804),
+ * its payload generated on the GPU with entropy object_entropy(seed_base, j):
+ *   S3DG_PAYLOAD_CONTROLLED  fill_controlled_data layout (data_gen.rs:151-224)
+ *   S3DG_PAYLOAD_RANDOM      generate_random_data layout (data_gen.rs:102-132)
+ *   S3DG_PAYLOAD_DGEN        the DG1 dgen-contract stream
+ * Parent directories are created; files are truncated.  max_in_flight writer
+ * threads (0 -> 64) write from a pinned host ring while the GPU generates the
+ * next chunk.  crc_out (nullable, n entries) receives the CRC-32 (crc32fast)
+ * of each whole file as written (StreamingDataWriter::checksum,
+ * src/streaming_writer.rs:183-186).  File-system errors -> S3DG_EIO. */
+enum { S3DG_PAYLOAD_CONTROLLED = 0, S3DG_PAYLOAD_RANDOM = 1, S3DG_PAYLOAD_DGEN = 2 };
+typedef struct {
+    uint64_t objects;       /* files written */
+    uint64_t bytes;         /* bytes written (payload + framing) */
+    double seconds;         /* wall time of the call */
+    double gpu_seconds;     /* time the generator thread waited on the GPU (gen + CRC + D2H) */
+} s3dg_put_stats;
+int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_t n, uint64_t size,
+                     int object_type, int payload, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                     uint64_t seed_base, uint32_t max_in_flight, uint32_t *crc_out,
+                     s3dg_put_stats *stats);
 
 /* ---- host-buffer drop-ins (src/data_gen.rs:151 signature) ---------------- */
 /* generate_random_data(size) (src/data_gen.rs:102): seeded analogue layout

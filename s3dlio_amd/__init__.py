@@ -21,4 +21,7 @@ from .objects import (Config, DataGenMode, ObjectType, build_npz, build_raw,  # 
                       build_tfrecord, build_tfrecord_with_index, generate_object,
                       generate_random_data, object_size)
 
+from .put import (DEFAULT_OBJECT_SIZE, PutResult, build_uri_list, put,  # noqa: F401
+                  put_objects, put_objects_with_random_data_and_type)
+
 __version__ = "0.1.0"

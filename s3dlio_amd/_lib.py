@@ -39,6 +39,12 @@ class ObjDesc(ctypes.Structure):
                 ("f_num", c_u32), ("f_den", c_u32)]
 
 
+class PutStats(ctypes.Structure):
+    """s3dg_put_stats"""
+    _fields_ = [("objects", c_u64), ("bytes", c_u64), ("seconds", ctypes.c_double),
+                ("gpu_seconds", ctypes.c_double)]
+
+
 # name -> (restype, argtypes); the exact export list of include/s3dlio_gpu.h
 SIGNATURES = {
     "s3dg_ctx_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
@@ -102,6 +108,8 @@ SIGNATURES = {
     "s3dg_npz_legacy_size": (c_int, [c_u64, c_u64, ctypes.POINTER(c_u64)]),
     "s3dg_build_npz": (c_int, [c_u64, c_vp, c_u64, c_vp, c_u64]),
     "s3dlio_generate_random_data": (c_int, [c_vp, ctypes.c_size_t]),
+    "s3dg_put_objects": (c_int, [c_vp, ctypes.POINTER(ctypes.c_char_p), c_u64, c_u64, c_int, c_int,
+                                 c_u64, c_u32, c_u32, c_u64, c_u32, c_vp, ctypes.POINTER(PutStats)]),
     "s3dg_last_error": (ctypes.c_char_p, []),
     "s3dg_version": (ctypes.c_char_p, []),
 }
@@ -126,6 +134,8 @@ def check(fn: str, code: int) -> None:
     if code != 0:
         if code == -1:
             raise ValueError((_L.s3dg_last_error() or b"").decode(errors="replace"))
+        if code == -4:   # S3DG_EIO
+            raise OSError((_L.s3dg_last_error() or b"").decode(errors="replace"))
         raise S3dgError(fn, code)
 
 

@@ -259,6 +259,41 @@ int s3dg_random_data(s3dg_ctx *c, void *dst, uint64_t len, uint64_t entropy, voi
     return S3DG_OK;
 }
 
+int s3dg_internal_ctx_device(s3dg_ctx *c, int *dev) {
+    if (int r = check_ctx(c)) return r;
+    *dev = c->device;
+    return S3DG_OK;
+}
+
+// Chunk of n_objs equal objects for the put pipeline: blocks [blk_lo, blk_hi)
+// of objects first_obj..first_obj+n_objs-1, object k's block blk_lo at
+// dst + k*stride; controlled layout or (random_layout) generate_random_data's.
+int s3dg_internal_fill_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride,
+                             uint64_t n_objs, uint64_t blk_lo, uint64_t blk_hi, int random_layout,
+                             uint64_t dedup, uint32_t f_num, uint32_t f_den, uint64_t seed_base,
+                             uint64_t first_obj, void *stream) {
+    if (int r = check_ctx(c)) return r;
+    if (obj_size == 0 || n_objs == 0) return S3DG_OK;
+    const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
+    if (blk_hi > nb) blk_hi = nb;
+    if (blk_lo >= blk_hi) return S3DG_OK;
+    if (!dst || !aligned16(dst) || (stride & 15u)) return fail(S3DG_EINVAL, "dst and stride must be 16-byte aligned");
+    PrefixParams pp{};
+    if (random_layout) {
+        if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+        pp.unique = 0xFFFFFFFFu;
+        pp.f_den = 0;
+        pp.m_unique = fastmod_magic(1);
+        pp.m_fden = fastmod_magic(1);
+    } else if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) {
+        return r;
+    }
+    HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, obj_size, stride, n_objs, (uint32_t)blk_lo,
+                               (uint32_t)blk_hi, seed_base, first_obj, pp, c->base_dev, (hipStream_t)stream),
+            "launch k_fill_stream(put chunk)");
+    return S3DG_OK;
+}
+
 int s3dg_fill_controlled(s3dg_ctx *c, void *dst, uint64_t len, uint64_t dedup, uint32_t f_num,
                          uint32_t f_den, uint64_t entropy, void *stream) {
     return s3dg_fill_controlled_range(c, dst, len, 0, ~0ull, dedup, f_num, f_den, entropy, stream);

@@ -47,13 +47,32 @@ __device__ __forceinline__ uint32_t mul_row(const uint32_t (*T)[256], uint32_t v
     return T[0][v & 0xFF] ^ T[1][(v >> 8) & 0xFF] ^ T[2][(v >> 16) & 0xFF] ^ T[3][v >> 24];
 }
 
-// One wave per region of `rows` 1 KiB rows (region = rows KiB, contiguous).
-// Lane l owns bytes [16 l, 16 l + 16) of every row: each row is one
-// coalesced 1 KiB load, and the lane keeps the Horner sum
+// One wave per region.  Segment s (s = 0..nseg-1) starts at src + s*seg_stride
+// and holds seg_rows whole 1 KiB rows; region k of a segment covers rows
+// [k*rows, min((k+1)*rows, seg_rows)).  Lane l owns bytes [16 l, 16 l + 16) of
+// every row: each row is one coalesced 1 KiB load, and the lane keeps the
+// Horner sum
 //   S_l = A^1024 S_l ^ raw16(piece)
 // so the region's raw CRC is XOR_l A^(16 (63 - l)) S_l.  Output: raw CRC per region.
-__global__ __launch_bounds__(256) void k_crc32_regions(const uint8_t *src, uint64_t nregions,
-                                                       uint32_t rows, const CrcTables *tabs,
+struct CrcSegArgs {
+    const uint8_t *src;
+    uint64_t nreg;          // nseg * regs_per_seg
+    uint64_t regs_per_seg;
+    uint64_t seg_stride;    // bytes
+    uint64_t seg_rows;      // whole 1 KiB rows per segment
+    uint32_t rows;          // rows per region
+};
+
+__device__ __forceinline__ uint32_t horner_row(const uint32_t (*trow)[256], const uint32_t (*tbyte)[256],
+                                               uint32_t S, const uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t c = mul_row(trow, S);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c ^= tbyte[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xFF];
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_crc32_regions(CrcSegArgs a, const CrcTables *tabs,
                                                        const uint32_t *lane_shift, uint32_t *out) {
     __shared__ CrcTables T;
     const uint32_t t = threadIdx.x, lane = t & 63;
@@ -64,25 +83,23 @@ __global__ __launch_bounds__(256) void k_crc32_regions(const uint8_t *src, uint6
     }
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * 4 + (t >> 6);
-    if (r >= nregions) return;
-    const uint4 *p = reinterpret_cast<const uint4 *>(src + r * (uint64_t)rows * 1024) + lane;
-    uint32_t S = 0;
-    for (uint32_t row = 0; row < rows; row += 4) {
+    if (r >= a.nreg) return;
+    const uint64_t seg = r / a.regs_per_seg, k = r - seg * a.regs_per_seg;
+    const uint64_t row0 = k * a.rows;
+    const uint32_t nrows = (uint32_t)((a.seg_rows - row0) < a.rows ? (a.seg_rows - row0) : a.rows);
+    const uint4 *p = reinterpret_cast<const uint4 *>(a.src + seg * a.seg_stride + row0 * 1024) + lane;
+    uint32_t S = 0, row = 0;
+    for (; row + 4 <= nrows; row += 4) {
         uint4 v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = p[(row + k) * 64];     // 4 rows in flight
+        for (int q = 0; q < 4; ++q) v[q] = p[(row + q) * 64];     // 4 rows in flight
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-            uint32_t c = mul_row(T.trow, S);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) c ^= T.tbyte[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xFF];
-            S = c;
-        }
+        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, v[q]);
     }
+    for (; row < nrows; ++row) S = horner_row(T.trow, T.tbyte, S, p[row * 64]);
     S = multmodp(lane_shift[lane], S);              // A^(16 (63 - lane))
 #pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) S ^= __shfl_xor(S, k);
+    for (int q = 32; q >= 1; q >>= 1) S ^= __shfl_xor(S, q);
     if (lane == 0) out[r] = S;
 }
 
@@ -157,68 +174,110 @@ uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
     return multmodp(x8n(len2), crc1) ^ crc2;
 }
 
-// CRC-32 of dev[0, len): device regions (raw CRCs) + host fold + host tail.
-//   std(M) = ~(A^n(~0) ^ raw(M)),   raw(M1||M2) = A^|M2| raw(M1) ^ raw(M2)
-hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_t *out,
-                        void **tab_cache, uint32_t **seg_cache, uint64_t *seg_cap) {
+hipError_t crc_tables_device(void **tab_cache) {
     static std::mutex init_mu;
     {
         std::lock_guard<std::mutex> g(init_mu);
         init_tables();
     }
-    uint32_t rows = 256;                                  // 256 KiB per wave region
-    while (len / ((uint64_t)rows * 1024) > (1ull << 20)) rows *= 2;
-    const uint64_t region = (uint64_t)rows * 1024;
-    const uint64_t nreg = len / region;
-    uint32_t raw = 0;
-    hipError_t e = hipSuccess;
-    if (nreg) {
-        if (!*tab_cache) {
-            if ((e = hipMalloc(tab_cache, sizeof(CrcTables) + 64 * 4)) != hipSuccess) return e;
-            if ((e = hipMemcpy(*tab_cache, &dev_tables_host, sizeof(CrcTables), hipMemcpyHostToDevice)) != hipSuccess)
-                return e;
-            if ((e = hipMemcpy((uint8_t *)*tab_cache + sizeof(CrcTables), lane_shift_host, 64 * 4,
-                               hipMemcpyHostToDevice)) != hipSuccess)
-                return e;
-        }
-        if (nreg > *seg_cap) {
-            if (*seg_cache) (void)hipFree(*seg_cache);
-            *seg_cache = nullptr;
-            *seg_cap = 0;
-            if ((e = hipMalloc(seg_cache, nreg * 4)) != hipSuccess) return e;
-            *seg_cap = nreg;
-        }
-        const uint64_t wgs = (nreg + 3) / 4;
-        (void)hipGetLastError();
-        hipLaunchKernelGGL(k_crc32_regions, dim3((uint32_t)wgs), dim3(256), 0, s, dev, nreg, rows,
-                           (const CrcTables *)*tab_cache,
-                           (const uint32_t *)((uint8_t *)*tab_cache + sizeof(CrcTables)), *seg_cache);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        std::vector<uint32_t> h(nreg);
-        if ((e = hipMemcpyAsync(h.data(), *seg_cache, nreg * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        // fold regions with a table-driven A^region multiply
+    if (*tab_cache) return hipSuccess;
+    hipError_t e;
+    if ((e = hipMalloc(tab_cache, sizeof(CrcTables) + 64 * 4)) != hipSuccess) return e;
+    if ((e = hipMemcpy(*tab_cache, &dev_tables_host, sizeof(CrcTables), hipMemcpyHostToDevice)) != hipSuccess)
+        return e;
+    return hipMemcpy((uint8_t *)*tab_cache + sizeof(CrcTables), lane_shift_host, 64 * 4,
+                     hipMemcpyHostToDevice);
+}
+
+CrcSegPlan crc_seg_plan(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride) {
+    CrcSegPlan P{};
+    P.nseg = nseg;
+    P.seg_len = seg_len;
+    P.seg_stride = seg_stride;
+    P.seg_rows = seg_len / 1024;
+    uint32_t rows = 256;                                   // 256 KiB per wave region
+    while (nseg * ((P.seg_rows + rows - 1) / rows) > (1ull << 24)) rows *= 2;
+    P.rows = rows;
+    P.regs_per_seg = (P.seg_rows + rows - 1) / rows;
+    P.nreg = nseg * P.regs_per_seg;
+    return P;
+}
+
+hipError_t crc_seg_launch(const CrcSegPlan &P, const uint8_t *dev, void *tab_dev, uint32_t *out_dev,
+                          hipStream_t s) {
+    if (P.nreg == 0) return hipSuccess;
+    CrcSegArgs a{dev, P.nreg, P.regs_per_seg, P.seg_stride, P.seg_rows, P.rows};
+    const uint64_t wgs = (P.nreg + 3) / 4;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(k_crc32_regions, dim3((uint32_t)wgs), dim3(256), 0, s, a, (const CrcTables *)tab_dev,
+                       (const uint32_t *)((uint8_t *)tab_dev + sizeof(CrcTables)), out_dev);
+    return hipGetLastError();
+}
+
+// Fold region raw CRCs into per-segment CRC-32s.  tails[s] points at the
+// segment's bytes past its whole rows (< 1 KiB, host memory), or is null when
+// seg_len is a multiple of 1 KiB.
+void crc_seg_fold(const CrcSegPlan &P, const uint32_t *regions, const uint8_t *const *tails,
+                  uint32_t *crcs) {
+    {
+        static std::mutex m;
+        std::lock_guard<std::mutex> g(m);
+        init_tables();
+    }
+    const uint64_t region = (uint64_t)P.rows * 1024;
+    const uint64_t last_rows = P.seg_rows - (P.regs_per_seg ? (P.regs_per_seg - 1) * P.rows : 0);
+    uint32_t Tr[4][256];
+    if (P.regs_per_seg > 1) {
         const uint32_t xr = x8n(region);
-        uint32_t Tr[4][256];
         for (int b = 0; b < 4; ++b)
             for (uint32_t x = 0; x < 256; ++x) Tr[b][x] = multmodp(xr, x << (8 * b));
-        for (uint64_t k = 0; k < nreg; ++k)
-            raw = (Tr[0][raw & 0xFF] ^ Tr[1][(raw >> 8) & 0xFF] ^ Tr[2][(raw >> 16) & 0xFF] ^
-                   Tr[3][raw >> 24]) ^ h[k];
     }
-    const uint64_t head = nreg * region;
-    uint32_t crc = nreg ? ~(multmodp(x8n(head), 0xFFFFFFFFu) ^ raw) : 0;
-    const uint64_t tail = len - head;
-    if (tail) {
-        std::vector<uint8_t> tb(tail);
-        if ((e = hipMemcpyAsync(tb.data(), dev + head, tail, hipMemcpyDeviceToHost, s)) != hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        const uint32_t ct = crc32_host_update(0, tb.data(), tail);
-        crc = nreg ? crc32_combine(crc, ct, tail) : ct;
+    const uint32_t x_last = x8n(last_rows * 1024);
+    const uint64_t head = P.seg_rows * 1024, tail = P.seg_len - head;
+    const uint32_t init = P.seg_rows ? multmodp(x8n(head), 0xFFFFFFFFu) : 0;
+    for (uint64_t sg = 0; sg < P.nseg; ++sg) {
+        uint32_t crc = 0;
+        if (P.seg_rows) {
+            const uint32_t *h = regions + sg * P.regs_per_seg;
+            uint32_t raw = 0;
+            for (uint64_t k = 0; k + 1 < P.regs_per_seg; ++k)
+                raw = (Tr[0][raw & 0xFF] ^ Tr[1][(raw >> 8) & 0xFF] ^ Tr[2][(raw >> 16) & 0xFF] ^
+                       Tr[3][raw >> 24]) ^ h[k];
+            raw = multmodp(x_last, raw) ^ h[P.regs_per_seg - 1];
+            crc = ~(init ^ raw);                          // std(M) = ~(A^n(~0) ^ raw(M))
+        }
+        if (tail) {
+            const uint32_t ct = crc32_host_update(0, tails[sg], tail);
+            crc = P.seg_rows ? crc32_combine(crc, ct, tail) : ct;
+        }
+        crcs[sg] = crc;
     }
-    *out = crc;
+}
+
+// CRC-32 of dev[0, len) (one segment): device regions + host fold + host tail.
+hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_t *out,
+                        void **tab_cache, uint32_t **seg_cache, uint64_t *seg_cap) {
+    hipError_t e;
+    if ((e = crc_tables_device(tab_cache)) != hipSuccess) return e;
+    const CrcSegPlan P = crc_seg_plan(1, len, len);
+    if (P.nreg > *seg_cap) {
+        if (*seg_cache) (void)hipFree(*seg_cache);
+        *seg_cache = nullptr;
+        *seg_cap = 0;
+        if ((e = hipMalloc(seg_cache, P.nreg * 4)) != hipSuccess) return e;
+        *seg_cap = P.nreg;
+    }
+    if ((e = crc_seg_launch(P, dev, *tab_cache, *seg_cache, s)) != hipSuccess) return e;
+    std::vector<uint32_t> h(P.nreg);
+    if (P.nreg && (e = hipMemcpyAsync(h.data(), *seg_cache, P.nreg * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return e;
+    const uint64_t head = P.seg_rows * 1024;
+    std::vector<uint8_t> tb(len - head);
+    if (!tb.empty() && (e = hipMemcpyAsync(tb.data(), dev + head, tb.size(), hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint8_t *tp = tb.data();
+    crc_seg_fold(P, h.data(), &tp, out);
     return hipSuccess;
 }
 

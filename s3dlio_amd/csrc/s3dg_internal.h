@@ -84,4 +84,23 @@ hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
                                 uint32_t pattern, hipStream_t s);
 
+
+// ---- CRC-32 (s3dg_crc.hip) -------------------------------------------------
+uint32_t crc32_host_update(uint32_t crc, const uint8_t *p, uint64_t n);
+uint32_t crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
+// nseg equal segments of seg_len bytes at seg_stride: whole 1 KiB rows are
+// hashed on the device (nreg regions of `rows` rows), the < 1 KiB tail of
+// each segment on the host.
+struct CrcSegPlan {
+    uint64_t nseg, seg_len, seg_stride, seg_rows, regs_per_seg, nreg;
+    uint32_t rows;
+};
+hipError_t crc_tables_device(void **tab_cache);
+CrcSegPlan crc_seg_plan(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride);
+hipError_t crc_seg_launch(const CrcSegPlan &P, const uint8_t *dev, void *tab_dev, uint32_t *out_dev,
+                          hipStream_t s);
+void crc_seg_fold(const CrcSegPlan &P, const uint32_t *regions, const uint8_t *const *tails,
+                  uint32_t *crcs);
+
 }  // namespace s3dg

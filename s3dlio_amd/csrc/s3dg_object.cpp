@@ -18,9 +18,6 @@
 #include <string>
 #include <vector>
 
-namespace s3dg {
-uint32_t crc32_host_update(uint32_t crc, const uint8_t *p, uint64_t n);
-}  // namespace s3dg
 
 extern "C" int s3dg_internal_fail(int code, const char *msg);
 extern "C" int s3dg_internal_random_host(uint8_t *buf, uint64_t len, uint64_t entropy,
@@ -58,6 +55,53 @@ uint64_t npz_legacy_size(uint64_t elements, uint64_t data_len) {
 
 }  // namespace
 
+namespace s3dg {
+
+// Framing around a payload of `len` bytes whose CRC-32 is `pcrc`:
+//   TFRECORD (one record)  u64 len | masked_crc(len) || payload || masked_crc(payload)
+//   NPZ (legacy)           local header | "data.npy" | NPY header || payload ||
+//                          central directory | EOCD
+//   RAW                    nothing
+void object_frame(int type, uint64_t elements, uint64_t len, uint32_t pcrc, std::vector<uint8_t> &pre,
+                  std::vector<uint8_t> &suf) {
+    pre.clear();
+    suf.clear();
+    if (type == S3DG_OBJ_TFRECORD) {
+        pre.resize(12);
+        put64(pre.data(), len);
+        put32(pre.data() + 8, mask_crc(crc32_host_update(0, pre.data(), 8)));   // tfrecord.rs:20-23
+        suf.resize(4);
+        put32(suf.data(), mask_crc(pcrc));                                      // :27-29
+    } else if (type == S3DG_OBJ_NPZ) {
+        const std::vector<uint8_t> h = npy_header_u1(elements);
+        const uint64_t npy = h.size() + len;
+        const uint32_t crc = crc32_combine(crc32_host_update(0, h.data(), h.size()), pcrc, len);
+        pre.resize(30 + kNameLen);
+        uint8_t *p = pre.data();                          // local file header
+        memcpy(p, "PK\x03\x04", 4);
+        put16(p + 4, 10); put16(p + 6, 0); put16(p + 8, 0); put16(p + 10, 0); put16(p + 12, 0x21);
+        put32(p + 14, crc); put32(p + 18, (uint32_t)npy); put32(p + 22, (uint32_t)npy);
+        put16(p + 26, kNameLen); put16(p + 28, 0);
+        memcpy(p + 30, kNpyName, kNameLen);
+        pre.insert(pre.end(), h.begin(), h.end());
+        const uint64_t cd_off = pre.size() + len;
+        suf.resize(46 + kNameLen + 22);
+        p = suf.data();                                   // central directory
+        memcpy(p, "PK\x01\x02", 4);
+        put16(p + 4, 20); put16(p + 6, 10); put16(p + 8, 0); put16(p + 10, 0); put16(p + 12, 0);
+        put16(p + 14, 0x21); put32(p + 16, crc); put32(p + 20, (uint32_t)npy); put32(p + 24, (uint32_t)npy);
+        put16(p + 28, kNameLen); put16(p + 30, 0); put16(p + 32, 0); put16(p + 34, 0); put16(p + 36, 0);
+        put32(p + 38, 0); put32(p + 42, 0);
+        memcpy(p + 46, kNpyName, kNameLen);
+        p += 46 + kNameLen;                               // end of central directory
+        memcpy(p, "PK\x05\x06", 4);
+        put16(p + 4, 0); put16(p + 6, 0); put16(p + 8, 1); put16(p + 10, 1);
+        put32(p + 12, 46 + kNameLen); put32(p + 16, (uint32_t)cd_off); put16(p + 20, 0);
+    }
+}
+
+}  // namespace s3dg
+
 extern "C" {
 
 int s3dg_build_tfrecord(uint64_t records, uint64_t record_size, const uint8_t *data, uint8_t *out,
@@ -91,32 +135,14 @@ int s3dg_npz_legacy_size(uint64_t elements, uint64_t data_len, uint64_t *out) {
 
 int s3dg_build_npz(uint64_t elements, const uint8_t *data, uint64_t data_len, uint8_t *out,
                    uint64_t out_len) {
-    const std::vector<uint8_t> h = npy_header_u1(elements);
     const uint64_t total = npz_legacy_size(elements, data_len);
     if (!out || out_len < total || (data_len && !data)) return s3dg_internal_fail(S3DG_EINVAL, "bad buffer");
-    const uint64_t npy = h.size() + data_len;
-    const uint64_t off_data = 30 + kNameLen + h.size();
+    std::vector<uint8_t> pre, suf;
+    const uint64_t off_data = 30 + kNameLen + npy_header_u1(elements).size();
     if (out + off_data != data) memmove(out + off_data, data, data_len);
-    memcpy(out + 30 + kNameLen, h.data(), h.size());
-    const uint32_t crc = crc32_host_update(crc32_host_update(0, h.data(), h.size()), out + off_data, data_len);
-    uint8_t *p = out;                                   // local file header
-    memcpy(p, "PK\x03\x04", 4);
-    put16(p + 4, 10); put16(p + 6, 0); put16(p + 8, 0); put16(p + 10, 0); put16(p + 12, 0x21);
-    put32(p + 14, crc); put32(p + 18, (uint32_t)npy); put32(p + 22, (uint32_t)npy);
-    put16(p + 26, kNameLen); put16(p + 28, 0);
-    memcpy(p + 30, kNpyName, kNameLen);
-    p = out + off_data + data_len;                      // central directory
-    memcpy(p, "PK\x01\x02", 4);
-    put16(p + 4, 20); put16(p + 6, 10); put16(p + 8, 0); put16(p + 10, 0); put16(p + 12, 0);
-    put16(p + 14, 0x21); put32(p + 16, crc); put32(p + 20, (uint32_t)npy); put32(p + 24, (uint32_t)npy);
-    put16(p + 28, kNameLen); put16(p + 30, 0); put16(p + 32, 0); put16(p + 34, 0); put16(p + 36, 0);
-    put32(p + 38, 0); put32(p + 42, 0);
-    memcpy(p + 46, kNpyName, kNameLen);
-    const uint64_t cd_off = off_data + data_len;
-    p += 46 + kNameLen;                                 // end of central directory
-    memcpy(p, "PK\x05\x06", 4);
-    put16(p + 4, 0); put16(p + 6, 0); put16(p + 8, 1); put16(p + 10, 1);
-    put32(p + 12, 46 + kNameLen); put32(p + 16, (uint32_t)cd_off); put16(p + 20, 0);
+    s3dg::object_frame(S3DG_OBJ_NPZ, elements, data_len, crc32_host_update(0, out + off_data, data_len), pre, suf);
+    memcpy(out, pre.data(), pre.size());
+    memcpy(out + off_data + data_len, suf.data(), suf.size());
     return S3DG_OK;
 }
 
