@@ -20,6 +20,7 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -386,8 +387,16 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
 // lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
 static int keystream_plan(s3dg_ctx *c, uint64_t chunk_bytes, KeystreamArgs &A, const uint64_t **jtab) {
     const uint64_t nd = chunk_bytes / 8;
-    uint32_t lpc = 1;   // as many lanes as keep >= 2048 draws per lane (jump cost <= 12.5 %)
-    while (lpc < 64 && nd / (2 * lpc) >= 2048) lpc *= 2;
+    // as many lanes per chunk as keep >= min_draws draws per lane (the jump
+    // costs 256 steps); up to 1024 lanes = 16 waves per chunk.
+    // S3DLIO_K2_MIN_DRAWS overrides the default (tuning experiments).
+    static const uint64_t min_draws = [] {
+        const char *e = getenv("S3DLIO_K2_MIN_DRAWS");
+        const long v = e ? atol(e) : 0;
+        return v >= 64 ? (uint64_t)v : (uint64_t)2048;
+    }();
+    uint32_t lpc = 1;
+    while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
     uint64_t span = (nd + lpc - 1) / lpc;
     span = (span + 15) / 16 * 16;
     if (span > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "chunk too large");
@@ -397,7 +406,7 @@ static int keystream_plan(s3dg_ctx *c, uint64_t chunk_bytes, KeystreamArgs &A, c
     const uint64_t key = ((uint64_t)lpc << 32) | span;
     auto it = c->jtabs.find(key);
     if (it == c->jtabs.end()) {
-        std::vector<uint64_t> h(4 * 64, 0);
+        std::vector<uint64_t> h(4 * (size_t)lpc, 0);
         for (uint32_t k = 0; k < lpc; ++k)
             if (!jump_poly((uint64_t)k * span, &h[4 * k]))
                 return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");

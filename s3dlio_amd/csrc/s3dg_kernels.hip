@@ -36,6 +36,18 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 
+// 64-bit rotate as two v_alignbit_b32 (the compiler emits shifts + ors):
+//   alignbit(a, b, s) = low 32 bits of ((a:b) >> s)
+template <int K>
+__device__ __forceinline__ uint64_t rotlk(uint64_t x) {
+    static_assert(K > 0 && K < 64 && K != 32, "rotate amount");
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (K > 32) { const uint32_t t = lo; lo = hi; hi = t; }
+    constexpr int k = K & 31;
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - k);
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - k);
+    return ((uint64_t)nhi << 32) | nlo;
+}
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) {
     return (x << k) | (x >> (64 - k));
 }
@@ -314,7 +326,7 @@ constexpr int kRowStride = 144;   // 128 B + 16 B pad: conflict-light ds_write_b
 
 __device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2, uint64_t &s3) {
     const uint64_t t = s1 << 17;
-    s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl64(s3, 45);
+    s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotlk<45>(s3);
 }
 
 __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
@@ -323,11 +335,13 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     uint8_t *myrows = rows[w];
     const uint32_t lpc = A.lpc, span = A.span;
-    const uint32_t cpw = 64 / lpc;                                   // chunks per wave
-    const uint64_t c0 = ((uint64_t)blockIdx.x * 4 + w) * cpw;
-    const uint64_t c = c0 + l / lpc;                                 // local chunk index
+    // global lane gl -> chunk gl / lpc, lane-in-chunk gl % lpc (lpc: power of two;
+    // lpc > 64 spreads one chunk over lpc/64 waves)
+    const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
+    const uint64_t gl = ((uint64_t)blockIdx.x * 4 + w) * 64 + l;
+    const uint64_t c = gl >> lsh;                                    // local chunk index
     const uint64_t cg = A.chunk0 + c;                                // chunk index in the object
-    const uint32_t sub = l % lpc;
+    const uint32_t sub = (uint32_t)(gl & (lpc - 1));
     const uint64_t coff = c * A.chunk_bytes;                         // offset within dst
     const uint64_t gofs = cg * A.chunk_bytes;                        // offset within the object
     const uint64_t clen = (c < A.nchunks && gofs < A.obj_len)
@@ -376,35 +390,65 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
     }
     const uint64_t d0 = (uint64_t)sub * span;                        // first draw index
     const uint32_t iters = span / 16;
+    // Wave-uniform fast paths: a 16-draw group needs no masking when no lane
+    // of the wave is inside a zero prefix or at its chunk's 1-4 byte tail;
+    // the stores need no guards when every region of the wave is full length.
+    const bool full_rows = __all(rlen == span * 8u);
+    // Per lane: iterations < it_plain may touch the zero prefix (draws below
+    // ceil(zlen/8)); iteration it_tail holds the 1-4 byte tail draw.
+    const uint64_t zdraws = (zlen + 7) >> 3;
+    const uint64_t zi = zdraws > d0 ? (zdraws - d0 + 15) / 16 : 0;
+    const uint32_t it_plain = zi < iters ? (uint32_t)zi : iters;
+    const uint32_t it_tail = (tail_hi && tail_draw >= d0 && tail_draw < d0 + span)
+                                 ? (uint32_t)((tail_draw - d0) / 16) : 0xFFFFFFFFu;
     for (uint32_t it = 0; it < iters; ++it) {
-        // 16 draws -> this lane's LDS row
+        const uint64_t dg = d0 + (uint64_t)it * 16;
+        if (__all(it >= it_plain && it != it_tail)) {
 #pragma unroll
-        for (int q = 0; q < 16; q += 2) {
-            uint64_t ra = rotl64(s0 + s3, 23) + s0; xo_step(s0, s1, s2, s3);
-            uint64_t rbv = rotl64(s0 + s3, 23) + s0; xo_step(s0, s1, s2, s3);
-            const uint64_t d = d0 + (uint64_t)it * 16 + q;
-            if (tail_hi && d == tail_draw) ra >>= 32;
-            if (tail_hi && d + 1 == tail_draw) rbv >>= 32;
-            if (8 * d < zlen) ra &= (8 * d + 8 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d)));
-            if (8 * d + 8 < zlen) rbv &= (8 * d + 16 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d - 8)));
-            *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
-                u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
+            for (int q = 0; q < 16; q += 2) {
+                const uint64_t ra = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
+                const uint64_t rbv = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
+                *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
+                    u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                uint64_t ra = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
+                uint64_t rbv = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
+                const uint64_t d = dg + q;
+                if (tail_hi && d == tail_draw) ra >>= 32;
+                if (tail_hi && d + 1 == tail_draw) rbv >>= 32;
+                if (8 * d < zlen) ra &= (8 * d + 8 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d)));
+                if (8 * d + 8 < zlen) rbv &= (8 * d + 16 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d - 8)));
+                *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
+                    u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t o = it * 128 + piece * 16;                   // offset within the row's region
+        if (full_rows) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint32_t r = 8 * i + (l >> 3);
-            if (o >= rrem[i]) continue;
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(myrows + r * kRowStride + piece * 16);
-            uint8_t *p = dst + raddr[i] + o;
-            if (o + 16 <= rrem[i]) {
-                *reinterpret_cast<u32x4 *>(p) = v;
-            } else {
-                const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-                for (uint32_t b = 0; b < 16 && o + b < rrem[i]; ++b) p[b] = (uint8_t)(dw[b >> 2] >> (8 * (b & 3)));
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t r = 8 * i + (l >> 3);
+                *reinterpret_cast<u32x4 *>(dst + raddr[i] + o) =
+                    *reinterpret_cast<const u32x4 *>(myrows + r * kRowStride + piece * 16);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t r = 8 * i + (l >> 3);
+                if (o >= rrem[i]) continue;
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(myrows + r * kRowStride + piece * 16);
+                uint8_t *p = dst + raddr[i] + o;
+                if (o + 16 <= rrem[i]) {
+                    *reinterpret_cast<u32x4 *>(p) = v;
+                } else {
+                    const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+                    for (uint32_t b = 0; b < 16 && o + b < rrem[i]; ++b) p[b] = (uint8_t)(dw[b >> 2] >> (8 * (b & 3)));
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -487,8 +531,7 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
                            hipStream_t s) {
     (void)hipGetLastError();
-    const uint64_t cpw = 64 / A.lpc;
-    const uint64_t waves = (A.nchunks + cpw - 1) / cpw;
+    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
     const uint64_t wgs = (waves + 3) / 4;
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_keystream, dim3((uint32_t)wgs), dim3(256), 0, s, dst, A, jtab);

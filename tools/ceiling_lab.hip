@@ -238,3 +238,59 @@ extern "C" __attribute__((visibility("default"))) int lab_v9(void *dst, uint64_t
     else hipLaunchKernelGGL(v10_ceiling_2d, dim3(nx, nb / nx), dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, 7u);
     return (int)hipGetLastError();
 }
+
+// V11: K2's store shape without the PRNG.  Each wave owns a chunk of 64 lane
+// regions of R bytes; iteration `it` writes `seg` bytes at offset it*seg of
+// every region, as seg/16 store instructions of (1024/seg) rows x seg bytes.
+// V12: each wave writes its 64*R chunk front to back, 1 KiB per instruction.
+template <int SEG, bool NT = false>
+__global__ __launch_bounds__(256) void v11_strided(uint8_t *dst, uint64_t nchunks, uint32_t R, uint32_t pat) {
+    const u32x4 v = {pat, pat + 1, pat + 2, pat + 3};
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t wv = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wv >= nchunks) return;
+    uint8_t *c = dst + wv * 64ull * R;
+    constexpr uint32_t lpr = SEG / 16, rpi = 1024 / SEG;
+    for (uint32_t it = 0; it < R / SEG; ++it)
+#pragma unroll
+        for (uint32_t i = 0; i < lpr; ++i) {
+            const uint32_t row = i * rpi + l / lpr;
+            st<NT>(c + (uint64_t)row * R + it * SEG + (l % lpr) * 16, v);
+        }
+}
+__global__ __launch_bounds__(256) void v12_wave_seq(uint8_t *dst, uint64_t nchunks, uint32_t R, uint32_t pat) {
+    const u32x4 v = {pat, pat + 1, pat + 2, pat + 3};
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t wv = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wv >= nchunks) return;
+    uint8_t *c = dst + wv * 64ull * R;
+    for (uint64_t o = 0; o < 64ull * R; o += 1024) st<false>(c + o + l * 16, v);
+}
+extern "C" __attribute__((visibility("default"))) int lab_v11(void *dst, uint64_t len, uint32_t R, int seg, void *s) {
+    const uint64_t nch = len / (64ull * R);
+    const dim3 g((uint32_t)((nch + 3) / 4));
+    switch (seg) {
+    case 64: hipLaunchKernelGGL(v11_strided<64>, g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u); break;
+    case 128: hipLaunchKernelGGL(v11_strided<128>, g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u); break;
+    case 256: hipLaunchKernelGGL(v11_strided<256>, g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u); break;
+    case 512: hipLaunchKernelGGL(v11_strided<512>, g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u); break;
+    case 1024: hipLaunchKernelGGL(v11_strided<1024>, g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u); break;
+    default: hipLaunchKernelGGL(v12_wave_seq, g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u); break;
+    }
+    return (int)hipGetLastError();
+}
+
+// V11 variants: nontemporal stores; occupancy forced down by dynamic LDS (lds_bytes per WG)
+extern "C" __attribute__((visibility("default"))) int lab_v11x(void *dst, uint64_t len, uint32_t R, int seg, int nt,
+                                                               uint32_t lds_bytes, void *s) {
+    const uint64_t nch = len / (64ull * R);
+    const dim3 g((uint32_t)((nch + 3) / 4));
+    if (nt) {
+        if (seg == 128) hipLaunchKernelGGL((v11_strided<128, true>), g, dim3(256), lds_bytes, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u);
+        else hipLaunchKernelGGL((v11_strided<512, true>), g, dim3(256), lds_bytes, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u);
+    } else {
+        if (seg == 128) hipLaunchKernelGGL((v11_strided<128, false>), g, dim3(256), lds_bytes, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u);
+        else hipLaunchKernelGGL((v11_strided<512, false>), g, dim3(256), lds_bytes, (hipStream_t)s, (uint8_t *)dst, nch, R, 7u);
+    }
+    return (int)hipGetLastError();
+}

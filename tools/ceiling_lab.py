@@ -25,7 +25,9 @@ def main():
         return
     import torch
     L = ctypes.CDLL(SO)
-    gib = float(sys.argv[1]) if len(sys.argv) > 1 else 16
+    L.lab_v11.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    gib = float(args[0]) if args else 16
     buf = torch.empty(int(gib * (1 << 30)), dtype=torch.uint8, device="cuda")
     n = buf.numel()
     p = buf.data_ptr()
@@ -39,6 +41,23 @@ def main():
     for nx in (2048, 256, 65536):
         V[f"v9 shared-chain 2D nx={nx}"] = (lambda x=nx: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), x, 0, ctypes.c_void_p(bp), ctypes.c_void_p(sh)))
         V[f"v10 ceiling 2D nx={nx}"] = (lambda x=nx: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), x, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh)))
+    if "--k2" in sys.argv:   # K2 store-shape study only
+        V.clear()
+        for R in (32768, 8192, 4096):
+            for seg in (128, 256, 512, 1024, 0):
+                if seg and R < seg:
+                    continue
+                name = f"v11 region={R} seg={seg}" if seg else f"v12 wave-seq chunk={64 * R}"
+                V[name] = (lambda r=R, g=seg: L.lab_v11(ctypes.c_void_p(p), ctypes.c_uint64(n), r, g, ctypes.c_void_p(sh)))
+        L.lab_v11x.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_uint32, ctypes.c_void_p]
+        for seg in (128, 512):
+            for nt in (0, 1):
+                for lds in (0, 40 * 1024, 80 * 1024, 150 * 1024):
+                    V[f"v11x region=32768 seg={seg} nt={nt} lds={lds}"] = (
+                        lambda g=seg, t=nt, d=lds: L.lab_v11x(ctypes.c_void_p(p), ctypes.c_uint64(n), 32768, g, t, d,
+                                                            ctypes.c_void_p(sh)))
+        V["v10 ceiling 2D nx=2048"] = lambda: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), 2048, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh))
     V["torch fill_"] = lambda: buf.fill_(7)
     res = {k: [] for k in V}
     for _ in range(5):
