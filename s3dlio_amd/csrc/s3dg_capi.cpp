@@ -443,25 +443,43 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
     return S3DG_OK;
 }
 
+int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride, uint64_t n_objs,
+                             uint64_t blk_lo, uint64_t blk_hi, uint64_t dedup, uint32_t f_num,
+                             uint32_t f_den, uint64_t seed_base, uint64_t first_obj, void *stream);
+
 int s3dg_dgen_fill(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t blk_lo, uint64_t blk_hi,
                    uint64_t dedup, uint32_t f_num, uint32_t f_den, uint64_t seed, void *stream) {
+    return s3dg_internal_dgen_chunk(c, dst, obj_size, 0, 1, blk_lo, blk_hi, dedup, f_num, f_den, seed, 0,
+                                    stream);
+}
+
+// n_objs equal DG1 objects in one launch: blocks [blk_lo, blk_hi) of object
+// first_obj + k at dst + k*stride, seeded object_entropy(seed_base, first_obj + k).
+int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride, uint64_t n_objs,
+                             uint64_t blk_lo, uint64_t blk_hi, uint64_t dedup, uint32_t f_num,
+                             uint32_t f_den, uint64_t seed_base, uint64_t first_obj, void *stream) {
     if (int r = check_ctx(c)) return r;
-    if (obj_size == 0) return S3DG_OK;
+    if (obj_size == 0 || n_objs == 0) return S3DG_OK;
     const uint64_t nb = (obj_size + kDgenBlock - 1) / kDgenBlock;
     if (blk_hi > nb) blk_hi = nb;
     if (blk_lo >= blk_hi) return S3DG_OK;
-    if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    if (!dst || !aligned16(dst) || (stride & 15u)) return fail(S3DG_EINVAL, "dst and stride must be 16-byte aligned");
+    const uint64_t span_bytes = (blk_hi * kDgenBlock < obj_size ? blk_hi * kDgenBlock : obj_size) - blk_lo * kDgenBlock;
+    if (n_objs > 1 && stride < span_bytes) return fail(S3DG_EINVAL, "stride too small: objects overlap");
     if (f_den == 0 || f_num >= f_den) return fail(S3DG_EINVAL, "need f_num < f_den");
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
     if (int r = keystream_plan(c, kDgenBlock, A, &jt)) return r;
     const uint64_t U = s3dg_unique_blocks(nb, dedup);
-    A.nchunks = blk_hi - blk_lo;
+    A.cpo = blk_hi - blk_lo;
+    A.nchunks = A.cpo * n_objs;
     A.chunk_bytes = kDgenBlock;
     A.obj_len = obj_size;
     A.chunk0 = blk_lo;
-    A.seed_base = seed;
+    A.obj_stride = stride;
+    A.seed_base = seed_base + (first_obj << 32);
+    A.seed_step = 1ull << 32;
     A.seed_mode = 1;
     A.unique = U == nb ? 0xFFFFFFFFu : (uint32_t)U;
     A.m_unique = fastmod_magic(U == nb ? 1u : (uint32_t)U);

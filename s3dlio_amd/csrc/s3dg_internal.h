@@ -76,6 +76,10 @@ struct KeystreamArgs {
     uint64_t m_unique;      // fastmod constant for U
     uint64_t zf_num, zf_den;  // zero prefix = floor(chunk_len * zf_num / zf_den)
     uint32_t lpc, span;     // lanes per chunk, draws per lane
+    // several objects per launch: chunk c -> object c / cpo (0 = one object),
+    // its chunk chunk0 + c % cpo, written at dst + object*obj_stride, seeded
+    // seed_base + object*seed_step
+    uint64_t cpo, obj_stride, seed_step;
 };
 
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,

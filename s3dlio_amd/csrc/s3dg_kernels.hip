@@ -340,9 +340,13 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
     const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
     const uint64_t gl = ((uint64_t)blockIdx.x * 4 + w) * 64 + l;
     const uint64_t c = gl >> lsh;                                    // local chunk index
-    const uint64_t cg = A.chunk0 + c;                                // chunk index in the object
+    const uint64_t cpo = A.cpo ? A.cpo : A.nchunks;
+    const uint64_t ko = c / cpo;                                     // object within the launch
+    const uint64_t cl = c - ko * cpo;
+    const uint64_t cg = A.chunk0 + cl;                               // chunk index in the object
     const uint32_t sub = (uint32_t)(gl & (lpc - 1));
-    const uint64_t coff = c * A.chunk_bytes;                         // offset within dst
+    const uint64_t coff = ko * A.obj_stride + cl * A.chunk_bytes;    // offset within dst
+    const uint64_t seed_base = A.seed_base + ko * A.seed_step;
     const uint64_t gofs = cg * A.chunk_bytes;                        // offset within the object
     const uint64_t clen = (c < A.nchunks && gofs < A.obj_len)
                               ? ((A.obj_len - gofs) < A.chunk_bytes ? (A.obj_len - gofs) : A.chunk_bytes)
@@ -358,10 +362,10 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
     // seed ^ (u * phi) with u = chunk % U (dedup)
     uint64_t x;
     if (A.seed_mode == 0) {
-        x = A.seed_base + cg;
+        x = seed_base + cg;
     } else {
         const uint32_t u = A.unique == 0xFFFFFFFFu ? (uint32_t)cg : fastmod((uint32_t)cg, A.m_unique, A.unique);
-        x = A.seed_base ^ ((uint64_t)u * 0x9E3779B97F4A7C15ull);
+        x = seed_base ^ ((uint64_t)u * 0x9E3779B97F4A7C15ull);
     }
     uint64_t s0 = mix64(x + 0x9E3779B97F4A7C15ull), s1 = mix64(x + 2 * 0x9E3779B97F4A7C15ull);
     uint64_t s2 = mix64(x + 3 * 0x9E3779B97F4A7C15ull), s3 = mix64(x + 4 * 0x9E3779B97F4A7C15ull);
