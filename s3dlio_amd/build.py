@@ -39,6 +39,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+           # kernel arguments preloaded into SGPRs (gfx950): the first scalar
+           # load of every 4 KiB-block workgroup disappears from its critical path
+           "-mllvm", "-amdgpu-kernarg-preload-count=16",
            "-I", os.path.join(ROOT, "include"), "-I", CSRC,
            "-DS3DG_BUILD", "-o", LIB] + SOURCES
     if verbose:

@@ -33,6 +33,7 @@
 namespace s3dg {
 namespace {
 
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 
@@ -224,23 +225,36 @@ __device__ __forceinline__ void write_block(uint8_t *bd, const BlockLds &S, int 
 }
 
 // The whole per-block body (all three phases); NW waves per 4 KiB block.
-template <bool NT, int NW>
+// Base-block pieces of thread t (issued first: they depend on kernel
+// arguments only, so their latency overlaps the plan's inputs).
+template <int NW>
+__device__ __forceinline__ void load_base(u32x4 (&B)[4 / NW], uint32_t t, const u32x4 *base) {
+    constexpr int T = 64 * NW;
+#pragma unroll
+    for (int k = 0; k < 4 / NW; ++k) B[k] = base[t + k * T];   // bytes 16(t+kT).. of the base block
+}
+
+template <int NW>
+__device__ __forceinline__ void store_image(BlockLds &S, uint32_t t, const u32x4 (&B)[4 / NW]) {
+    constexpr int T = 64 * NW;
+#pragma unroll
+    for (int k = 0; k < 4 / NW; ++k)
+        *reinterpret_cast<u32x4 *>(S.img + 16 * (t + k * T)) = B[k];   // :205-207
+}
+
+// IMG: the caller has already written the base image into S (batch kernel).
+template <bool NT, int NW, bool IMG = false>
 __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, uint32_t wave,
                                           uint32_t i, uint64_t size, uint64_t entropy,
-                                          const PrefixParams &pp, const u32x4 *base) {
+                                          const PrefixParams &pp, const u32x4 (&B)[4 / NW]) {
     constexpr int T = 64 * NW, SPL = 4 / NW;   // segments per lane
     const uint32_t lane = t & 63;
-    u32x4 B[SPL];
-#pragma unroll
-    for (int k = 0; k < SPL; ++k) B[k] = base[t + k * T];   // bytes 16(t+kT).. of the base block
     Plan P;
     if (wave == 0) {
         plan_block(P, lane, i, size, entropy, pp);
         if (lane == 0) { S.meta[0] = P.c; S.meta[1] = P.L; }
     }
-#pragma unroll
-    for (int k = 0; k < SPL; ++k)
-        *reinterpret_cast<u32x4 *>(S.img + 16 * (t + k * T)) = B[k];   // :205-207
+    if constexpr (!IMG) store_image<NW>(S, t, B);
     __syncthreads();
 #if !(S3DG_ABLATE & 1)
     if (wave == 0) patch_image(S, P, lane);
@@ -264,8 +278,10 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t 
     uint64_t jv = j;                 // block address on the VALU: keep the scalar unit
     asm volatile("" : "+v"(jv));     // for the PRNG chain
     uint8_t *bd = dst + jv * stride + (uint64_t)blockIdx.x * kBlk;
+    u32x4 B[4 / NW];
+    load_base<NW>(B, t, base);
     gen_block<NT, NW>(bd, S, t, wave, blk_lo + blockIdx.x, obj_size,
-                  seed_base + ((first_obj + j) << 32), pp, base);
+                      seed_base + ((first_obj + j) << 32), pp, B);
 }
 
 // Batch: workgroup g -> tile record g/64 (one scalar load), block
@@ -277,12 +293,23 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t g = g0 + blockIdx.x;
-    const TileRec e = tiles[g >> 6];
+    // The tile record (64 B) in ONE scalar load, issued first; then the base
+    // block's vector loads and its LDS image, so the two memory latencies
+    // overlap instead of following each other (the compiler otherwise splits
+    // the record into four loads around the early-exit branch).
+    u32x16 raw;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + (g >> 6)) : "memory");
+    u32x4 B[4 / NW];
+    load_base<NW>(B, t, base);
+    store_image<NW>(S, t, B);
+    // the wait "redefines" raw, so no use of the record can move above it
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(raw) :: "memory");
+    const TileRec e = __builtin_bit_cast(TileRec, raw);
     const uint32_t k = (uint32_t)(g & 63);
     const uint64_t ib = (uint64_t)e.first + k;
     if (ib * kBlk >= e.size) return;               // uniform for the whole workgroup
-    gen_block<NT, NW>(dst_base + e.dst_off + (uint64_t)k * kBlk, S, t, wave, (uint32_t)ib, e.size,
-                      e.entropy, e.pp, base);
+    gen_block<NT, NW, true>(dst_base + e.dst_off + (uint64_t)k * kBlk, S, t, wave, (uint32_t)ib, e.size,
+                            e.entropy, e.pp, B);
 }
 
 // tiles[tile] = record of every 64-block tile of every object.
