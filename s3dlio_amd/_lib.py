@@ -20,7 +20,7 @@ except Exception:  # pragma: no cover - torch is optional for the product
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libs3dlio_amd.so")
+LIB_PATH = os.environ.get("S3DLIO_AMD_LIB") or os.path.join(HERE, "libs3dlio_amd.so")   # override: A/B diagnostics
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -358,9 +358,6 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         // only on its own stream, so drain the device before freeing
         HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
         if (c->tile_obj) (void)hipFree(c->tile_obj);
-    for (auto &kv : c->jtabs) (void)hipFree(kv.second);
-    if (c->crc_tab) (void)hipFree(c->crc_tab);
-    if (c->crc_seg) (void)hipFree(c->crc_seg);
         c->tile_obj = nullptr; c->tile_cap = 0;
         const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
         HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");

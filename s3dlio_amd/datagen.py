@@ -30,6 +30,7 @@ import os
 
 import numpy as np
 
+from . import hostbuf
 from ._lib import c_u64, c_vp, call, lib
 from .device import compress_ratio
 
@@ -85,14 +86,14 @@ class _Gen:
 
 
 def _new_bytes(size: int, dedup: int, compress, seed: int | None) -> memoryview:
-    out = np.empty(size, np.uint8)           # every byte is written by the generator
+    out = hostbuf.empty(size)                # every byte is written by the generator
     if size:
         g = _Gen(size, dedup, compress, seed)
         try:
             g.fill(int(out.ctypes.data), size)
         finally:
             g.close()
-    return memoryview(out).toreadonly()      # BytesView: read-only, zero-copy buffer
+    return hostbuf.readonly(out)             # BytesView: read-only, zero-copy buffer
 
 
 # ---- PyO3 surface --------------------------------------------------------------

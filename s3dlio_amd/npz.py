@@ -13,6 +13,7 @@ import threading
 
 import numpy as np
 
+from . import hostbuf
 from ._lib import c_u32, c_u64, call, lib
 from .device import Context, _ptr, _stream
 
@@ -47,13 +48,13 @@ def generate_npz_bytes(shape, dtype: str = "<f4", num_samples: int = 1):
     """Return the NPZ archive as a read-only zero-copy buffer (BytesView)."""
     arr, nd = _shape_arr(shape)
     total = npz_size(shape, dtype, num_samples)
-    out = np.empty(total, np.uint8)          # every byte is written by the builder
+    out = hostbuf.empty(total)               # every byte is written by the builder
     try:
         call("s3dg_npz_build", default_context()._h, arr, nd, dtype.encode(), int(num_samples),
              int(out.ctypes.data), total)
     except Exception as e:   # the reference maps errors to RuntimeError (:409)
         raise RuntimeError(str(e)) from e
-    return memoryview(out).toreadonly()
+    return hostbuf.readonly(out)
 
 
 def crc32_device(ctx: Context, dst, nbytes: int | None = None, stream=None) -> int:

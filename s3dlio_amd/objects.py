@@ -17,6 +17,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
+from . import hostbuf
 from ._lib import c_u64, call
 
 
@@ -81,13 +82,14 @@ def generate_object(cfg: Config, seed: int | None = None):
     """Build one object payload (read-only buffer).  seed=None reproduces the
     reference's non-deterministic entropy; an int makes it reproducible."""
     n = object_size(cfg.object_type, cfg.elements, cfg.element_size)
-    out = np.empty(max(n, 1), np.uint8)
+    out = hostbuf.empty(n)
     w = c_u64()
     call("s3dg_generate_object", int(cfg.object_type), cfg.elements, cfg.element_size,
          1 if cfg.use_controlled else 0, max(0, cfg.dedup_factor), max(0, cfg.compress_factor),
          int(cfg.data_gen_mode), 0 if seed is None else 1,
-         0 if seed is None else int(seed) & (2**64 - 1), int(out.ctypes.data), n, ctypes.byref(w))
-    return memoryview(out[:n]).toreadonly()
+         0 if seed is None else int(seed) & (2**64 - 1), int(out.ctypes.data) if n else 0, n,
+         ctypes.byref(w))
+    return hostbuf.readonly(out)
 
 
 def generate_random_data(size: int) -> bytes:

@@ -70,6 +70,39 @@ def _frame(t, size, payload):
     return payload
 
 
+def _dump_failure(oracle, kind, t, size, d, c, seed, j, got, pay, bad):
+    """Diagnostics for a payload mismatch (written under gpurun_out/ when present)."""
+    import json
+    from s3dlio_amd import compress_ratio
+    info = {"case": [kind, t, size, d, c, seed, j], "ndiff": int(bad.size), "first": bad[:8].tolist()}
+    off = len(got) - size - (4 if t == "TFRECORD" else 0) - (76 if t == "NPZ" else 0)
+    off = {"RAW": 0, "TFRECORD": 12}.get(t, off)
+    gp = np.frombuffer(got[off:off + size], np.uint8)
+    info["payload_equal"] = gp.tobytes() == pay
+    fn, fd = compress_ratio(max(1, c))
+    hits = []
+    if kind == "dgen":
+        for dj in range(-3, 4):
+            e2 = oracle.object_entropy(seed, j + dj) if j + dj >= 0 else None
+            if e2 is not None and oracle.dgen_fill(size, max(1, d), fn, fd, e2).tobytes() == gp.tobytes():
+                hits.append(f"dgen seed of object {j + dj}")
+        xs = oracle.xoshiro_chunks(size, 1 << 20, oracle.object_entropy(seed, j)).tobytes()
+        if xs == gp.tobytes():
+            hits.append("seed_mode 0")
+    info["matches"] = hits
+    info["got_zero_frac"] = float((gp == 0).mean())
+    blk = 1 << 20
+    nb = (size + blk - 1) // blk
+    per_block = []
+    for b in range(nb):
+        a, z = b * blk, min(size, (b + 1) * blk)
+        per_block.append(int(np.count_nonzero(gp[a:z] != np.frombuffer(pay[a:z], np.uint8))))
+    info["diff_per_MiB_block"] = per_block[:64]
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/put_fail_{kind}_{t}_{j}.json", "w") as f:
+        json.dump(info, f)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,t,n,size,d,c", [
     ("controlled", "RAW", 70, 3 * MiB + 5, 2, 3),     # 3 chunks of packed objects, ragged size
@@ -90,8 +123,15 @@ def test_gpu_put_round_trip(S, oracle, golden_base, gpu_ctx, tmp_path, kind, t, 
     for j in range(n):
         got = open(f"{tmp_path}/sub/dir/obj-{j}", "rb").read()
         assert len(got) == framed
-        exp = _frame(t, size, _expect(oracle, golden_base, kind, size, d, c, seed, j))
-        assert got == exp, f"object {j}"
+        pay = _expect(oracle, golden_base, kind, size, d, c, seed, j)
+        exp = _frame(t, size, pay)
+        if got != exp:
+            g, e = np.frombuffer(got, np.uint8), np.frombuffer(exp, np.uint8)
+            bad = np.nonzero(g != e)[0]
+            _dump_failure(oracle, kind, t, size, d, c, seed, j, got, pay, bad)
+            raise AssertionError(f"object {j}: {bad.size} bytes differ, first at {bad[:4].tolist()}; "
+                                 f"file crc {zlib.crc32(got):08x} returned {r.checksums[j]:08x} "
+                                 f"payload crc expected {zlib.crc32(pay):08x}")
         assert r.checksums[j] == zlib.crc32(got)
     assert r.checksum_str(0).startswith("crc32c:")
 
