@@ -13,7 +13,8 @@ from .datagen import (DataGenerator, Generator, ObjectGen, default_data_gen_thre
                       generate_controlled_data_alt, generate_controlled_data_streaming,
                       generate_data, generate_data_with_threads, generate_into_buffer,
                       optimal_chunk_size, py_default_data_gen_threads, py_total_cpus,
-                      total_cpus)
+                      total_cpus, NumaMode, GeneratorConfig, DataBuffer, ObjectGenAlt,
+                      generate_data_from_config, generate_data_simple, generate_data_with_config)
 
 from .npz import crc32_combine, crc32_device, generate_npz_bytes, npz_size  # noqa: F401
 

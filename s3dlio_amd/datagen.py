@@ -257,3 +257,111 @@ def optimal_chunk_size(total_size: int) -> int:
         if total_size >= lim:
             return lim
     return total_size
+
+
+# ---- data_gen_alt / dgen-data re-exports (src/data_gen_alt.rs:14-150) --------------
+
+import enum as _enum
+from dataclasses import dataclass as _dataclass
+
+
+class NumaMode(_enum.Enum):
+    """dgen_data::NumaMode -- accepted for signature compatibility; generation runs
+    on the GPU, so there is no host NUMA placement to choose."""
+    AUTO = "auto"
+    FORCE = "force"
+    DISABLED = "disabled"
+
+
+@_dataclass
+class GeneratorConfig:
+    """dgen_data::GeneratorConfig (fields: python_datagen_api.rs:59-68)."""
+    size: int
+    dedup_factor: int = 1
+    compress_factor: int = 1
+    numa_mode: NumaMode = NumaMode.AUTO
+    max_threads: int | None = None
+    numa_node: int | None = None
+    block_size: int | None = None
+    seed: int | None = None
+
+    def _check(self):
+        if self.block_size not in (None, DGEN_BLOCK_SIZE):
+            raise ValueError(f"block_size must be {DGEN_BLOCK_SIZE} (the DG1 layout's 1 MiB blocks)")
+        if self.size < 0:
+            raise ValueError("size must be >= 0")
+
+
+class DataBuffer:
+    """dgen_data::DataBuffer: owned generated bytes (.into_bytes(), .as_slice(), .as_ptr())."""
+
+    def __init__(self, view: memoryview):
+        self._v = view
+
+    def into_bytes(self) -> memoryview:
+        return self._v
+
+    def as_slice(self) -> memoryview:
+        return self._v
+
+    def as_ptr(self) -> int:
+        return int(np.frombuffer(self._v, np.uint8).ctypes.data) if self._v.nbytes else 0
+
+    def __len__(self) -> int:
+        return self._v.nbytes
+
+    def __bytes__(self) -> bytes:
+        return self._v.tobytes()
+
+
+def generate_data_from_config(config: GeneratorConfig) -> DataBuffer:
+    """dgen_data::generate_data(GeneratorConfig) -> DataBuffer.  Unlike the
+    reference's batch path (data_gen_alt.rs:63-64) the seed is honoured."""
+    config._check()
+    return DataBuffer(_new_bytes(config.size, max(1, config.dedup_factor),
+                                 max(1, config.compress_factor), config.seed))
+
+
+def generate_data_simple(size: int, dedup: int, compress: int) -> DataBuffer:
+    """dgen_data::generate_data_simple."""
+    return generate_data_from_config(GeneratorConfig(size, dedup, compress))
+
+
+def generate_data_with_config(config: GeneratorConfig) -> memoryview:
+    """src/data_gen_alt.rs:56-59 (Bytes = read-only zero-copy view)."""
+    return generate_data_from_config(config).into_bytes()
+
+
+class ObjectGenAlt:
+    """src/data_gen_alt.rs:89-149: streaming generator over one object,
+    fill_chunk(buf) writes into `buf` and returns the byte count (0 when done)."""
+
+    def __init__(self, total_size: int, dedup: int, compress: int, seed: int | None = None):
+        if seed is None:   # :98-104 system-time seed
+            import time
+            seed = time.time_ns() & (2**64 - 1)
+        self._g = _Gen(total_size, max(1, dedup), max(1, compress), seed)
+
+    @classmethod
+    def new(cls, total_size: int, dedup: int, compress: int) -> "ObjectGenAlt":
+        return cls(total_size, dedup, compress)
+
+    @classmethod
+    def new_with_seed(cls, total_size: int, dedup: int, compress: int, seed: int) -> "ObjectGenAlt":
+        return cls(total_size, dedup, compress, seed)
+
+    def fill_chunk(self, buf) -> int:
+        ptr, n = _writable(buf)
+        return self._g.fill(ptr, n) if n else 0
+
+    def is_complete(self) -> bool:
+        return bool(lib.s3dg_gen_is_complete(self._g.h))
+
+    def reset(self) -> None:
+        call("s3dg_gen_reset", self._g.h)
+
+    def position(self) -> int:
+        return int(lib.s3dg_gen_position(self._g.h))
+
+    def total_size(self) -> int:
+        return int(lib.s3dg_gen_total_size(self._g.h))

@@ -117,3 +117,12 @@ def test_dg1_oracles_agree():
     for (n, d, fn, fd, s) in [(3 * 2**20 + 5, 1, 0, 1, 7), (2**20 * 5 + 9, 2, 1, 2, 99),
                               (100, 3, 2, 3, 5), (2**20, 1, 0, 1, 2**64 - 1), (7, 0, 1, 3, 1)]:
         assert bytes(C.dgen_fill(n, d, fn, fd, s)) == P.dgen_fill(n, d, fn, fd, s)
+
+
+def test_generator_config_validation_cpu():
+    """Host-side checks happen before any GPU work (block size is fixed by DG1)."""
+    import s3dlio_amd as S
+    c = S.GeneratorConfig(1000)
+    assert (c.dedup_factor, c.compress_factor, c.numa_mode, c.seed) == (1, 1, S.NumaMode.AUTO, None)
+    with pytest.raises(ValueError, match="block_size"):
+        S.generate_data_from_config(S.GeneratorConfig(10, block_size=4096))

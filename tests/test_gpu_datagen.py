@@ -212,3 +212,36 @@ def test_thread_safety_eight_generators(S):
         b = bytearray(3 * MiB)
         S.Generator(3 * MiB, seed=k).fill_chunk(b)
         assert sha(b) == res[k]
+
+
+# ---- data_gen_alt surface (src/data_gen_alt.rs:14-150) ------------------------------
+
+@pytest.mark.gpu
+def test_generate_data_with_config_and_databuffer(S, oracle):
+    n = 3 * (1 << 20) + 11
+    cfg = S.GeneratorConfig(n, dedup_factor=2, compress_factor=3, seed=4242)
+    buf = S.generate_data_from_config(cfg)
+    assert len(buf) == n and buf.as_ptr() != 0
+    fn, fd = S.compress_ratio(3)
+    assert bytes(buf) == oracle.dgen_fill(n, 2, fn, fd, 4242).tobytes()
+    assert bytes(S.generate_data_with_config(cfg)) == bytes(buf.into_bytes())
+    assert bytes(S.generate_controlled_data_alt(n, 2, 3, seed=4242)) == bytes(buf.as_slice())
+    assert len(S.generate_data_simple(777, 1, 1)) == 777
+
+
+@pytest.mark.gpu
+def test_object_gen_alt_streaming(S):
+    n = 5 * (1 << 20) + 3
+    g = S.ObjectGenAlt.new_with_seed(n, 2, 2, 99)
+    whole = bytes(S.generate_data_from_config(S.GeneratorConfig(n, 2, 2, seed=99)))
+    parts, b = [], bytearray(1 << 20)
+    while not g.is_complete():
+        k = g.fill_chunk(b)
+        parts.append(bytes(b[:k]))
+    assert b"".join(parts) == whole and g.position() == g.total_size() == n
+    assert g.fill_chunk(b) == 0
+    g.reset()
+    assert g.position() == 0 and not g.is_complete()
+    a1 = S.ObjectGenAlt.new(4096, 1, 1)                  # system-time seed (data_gen_alt.rs:98-104)
+    x = bytearray(4096)
+    assert a1.fill_chunk(x) == 4096 and a1.is_complete()
