@@ -78,6 +78,10 @@ def parse():
                    help="device output ring per GPU (objects wrap when the step exceeds it)")
     p.add_argument("--waves-per-block", type=int, default=None, help="1, 2 or 4 (default 2)")
     p.add_argument("--nt-stores", action="store_true", help="nontemporal stores (default plain)")
+    p.add_argument("--occupancy", type=int, default=None,
+                   help="resident fill workgroups per CU cap (default: library's, 12 stream / none batch)")
+    p.add_argument("--prefetch", type=int, default=None,
+                   help="batch tile-record prefetch distance in tiles (default: library's, 128)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")
@@ -105,6 +109,10 @@ def main() -> int:
     cfg = CONFIGS[args.config]
     ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block,
                   nontemporal=args.nt_stores)
+    if args.occupancy is not None:
+        ctx.set_occupancy(args.occupancy, args.occupancy)
+    if args.prefetch is not None:
+        ctx.set_batch_prefetch(args.prefetch)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     fn, fd = compress_ratio(cfg["compress"])
@@ -160,6 +168,13 @@ def main() -> int:
             launches.append(("batch", arr, b1 - b0))
         step_bytes = sum(sizes)
     base_ptr = int(ring.data_ptr())
+    batch = cfg["size"] is None
+    if cfg.get("keystream"):
+        launch_shape = "one wave per 2 MiB chunk (64 lanes x 4096 draws, jump-ahead)"
+    else:
+        waves = args.waves_per_block or (1 if batch else 2)
+        launch_shape = (f"one {64 * waves}-thread workgroup per 4 KiB block, "
+                        f"{ctx.query_occupancy(batch=batch)} resident per CU")
 
     def step(evs=None):
         for L in launches:
@@ -231,16 +246,31 @@ def main() -> int:
         if not verified:
             print("bench: VERIFICATION FAILED: sampled objects differ from the oracle", file=sys.stderr)
 
-    # ---- write-only ceiling on the same buffer (same store path) -----------------------
+    # ---- write-only ceiling on the same buffer -----------------------------------------
+    # a store-only kernel (one 4 KiB chunk per workgroup, 16-byte stores) in the
+    # stream fill kernel's launch shape and in the shapes that measured fastest
+    # for pure stores on MI355X (tools/batch_lab.py); the largest is the ceiling
     ceil_bytes = min(int(ring.numel()), 16 * GiB) // 4096 * 4096
-    ctx.write_ceiling(ring, ceil_bytes, stream=stream)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(3):
+
+    def ceiling_rate():
         ctx.write_ceiling(ring, ceil_bytes, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ceiling_gbs = 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            ctx.write_ceiling(ring, ceil_bytes, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    ceil_shapes = {}
+    for waves, occ in [(args.waves_per_block or 2, -1 if args.occupancy is None else args.occupancy),
+                       (4, 0), (4, 4), (4, 3), (2, 4)]:
+        ctx.set_waves_per_block(waves)
+        ctx.set_occupancy(occ, occ)
+        ceil_shapes[f"{waves}w_{ctx.query_occupancy()}perCU"] = round(ceiling_rate(), 1)
+    ceiling_gbs = max(ceil_shapes.values())
+    ctx.set_waves_per_block(args.waves_per_block or 0)
+    occ = -1 if args.occupancy is None else args.occupancy
+    ctx.set_occupancy(occ, occ)
 
     # ---- D2H-inclusive rate (bounded sample; never `value`) -------------------------------
     d2h = None
@@ -275,11 +305,11 @@ def main() -> int:
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic_from_profiles(args.config, int(sum(launch_bytes) / len(launch_bytes))),
                          "kernel": "k_keystream" if cfg.get("keystream") else ("k_fill_stream" if cfg["size"] else "k_fill_batch"),
-                         "launch_shape": ("one wave per 2 MiB chunk (64 lanes x 4096 draws, jump-ahead)" if cfg.get("keystream")
-                                          else f"one {64 * (args.waves_per_block or 2)}-thread workgroup per 4 KiB block"),
+                         "launch_shape": launch_shape,
                          "avg_launch_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": int(sum(launch_bytes) / len(launch_bytes)),
                          "write_ceiling_GBps": round(ceiling_gbs, 1),
+                         "write_ceiling_shapes_GBps": ceil_shapes,
                          "frac_of_write_ceiling": round(achieved_gbs / ceiling_gbs, 4)},
             "cpu_baseline": cpu,
             "d2h_inclusive": d2h,

@@ -69,6 +69,15 @@ int s3dg_get_base_block(s3dg_ctx *ctx, uint8_t *out4096);
 int s3dg_set_waves_per_block(s3dg_ctx *ctx, int waves);
 /* 1 = nontemporal stores, 0 = plain stores (default). */
 int s3dg_set_nontemporal(s3dg_ctx *ctx, int on);
+/* Cap on resident fill workgroups per CU (reserved LDS), for stream and
+ * batch launches separately; 0 = hardware maximum, negative = the default.
+ * Defaults 12 (stream) and 0 (batch), measured on MI355X.  A tuning knob; results are identical. */
+int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_cu);
+/* Batch launches: distance (in 64-block tiles) at which workgroups warm the
+ * L2 with a later tile record; 0 = off.  Default 128.  Results are identical. */
+int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
+/* Resident workgroups per CU the current settings give (HIP occupancy API). */
+int s3dg_query_occupancy(s3dg_ctx *ctx, int batch, int *wgs_per_cu);
 
 /* ---- parameter helpers (host math shared with the kernels) --------------- */
 uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup);

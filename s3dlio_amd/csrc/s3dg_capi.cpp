@@ -29,10 +29,16 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 
 using namespace s3dg;
 
+constexpr int kDefaultOccStream = 12, kDefaultOccBatch = 0;
+
 struct s3dg_ctx {
     int device = 0;
     bool nontemporal = false;          // plain stores measured faster
     int waves_per_block = 0;           // 0 = auto: 2 for streams, 1 for batches (measured)
+    // resident fill workgroups per CU (0 = hardware max); measured on MI355X
+    // (DESIGN.md §5.1): 12 for 2-wave stream blocks, no cap for 1-wave batch blocks
+    int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
+    uint32_t prefetch_tiles = 128;     // batch tile-record prefetch distance
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // batch descriptor table (device) + pinned staging, grown on demand
@@ -118,6 +124,8 @@ LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false) {
     LaunchCfg lc;
     lc.nontemporal = c->nontemporal;
     lc.waves_per_block = c->waves_per_block ? c->waves_per_block : (batch ? 1 : 2);
+    lc.dyn_lds = occupancy_lds(batch ? c->occ_batch : c->occ_stream, kFillStaticLds);
+    lc.prefetch_tiles = batch ? c->prefetch_tiles : 0;
     return lc;
 }
 
@@ -222,6 +230,28 @@ int s3dg_set_waves_per_block(s3dg_ctx *c, int waves) {
 int s3dg_set_nontemporal(s3dg_ctx *c, int on) {
     if (!c) return fail(S3DG_EINVAL, "null context");
     c->nontemporal = on != 0;
+    return S3DG_OK;
+}
+
+int s3dg_set_occupancy(s3dg_ctx *c, int stream_wgs_per_cu, int batch_wgs_per_cu) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (stream_wgs_per_cu > 40 || batch_wgs_per_cu > 40)
+        return fail(S3DG_EINVAL, "workgroups per CU must be at most 40");
+    c->occ_stream = stream_wgs_per_cu < 0 ? kDefaultOccStream : stream_wgs_per_cu;
+    c->occ_batch = batch_wgs_per_cu < 0 ? kDefaultOccBatch : batch_wgs_per_cu;
+    return S3DG_OK;
+}
+
+int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    c->prefetch_tiles = tiles;
+    return S3DG_OK;
+}
+
+int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
+    if (int r = check_ctx(c)) return r;
+    if (!wgs_per_cu) return fail(S3DG_EINVAL, "null output");
+    HIP_TRY(fill_occupancy(cfg_for(c, batch != 0), batch != 0, wgs_per_cu), "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     return S3DG_OK;
 }
 

@@ -52,7 +52,15 @@ static_assert(sizeof(TileRec) == 64, "TileRec is one s_load_dwordx16");
 struct LaunchCfg {
     bool nontemporal;
     int waves_per_block;   // 1, 2 or 4 wave64s per 4 KiB block (one workgroup)
+    uint32_t dyn_lds = 0;  // reserved dynamic LDS per workgroup (occupancy cap)
+    uint32_t prefetch_tiles = 0;   // batch: tile-record prefetch distance (0 = off)
 };
+
+// Dynamic LDS that caps a fill launch at `wgs` resident workgroups per CU
+// (0 = no cap).  Static LDS of the fill kernels: one BlockLds per block.
+uint32_t occupancy_lds(int wgs, uint32_t static_lds);
+constexpr uint32_t kFillStaticLds = kBlk + 16;
+hipError_t fill_occupancy(const LaunchCfg &lc, bool batch, int *wgs_per_cu);
 
 hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size,
                               uint64_t stride, uint64_t n_objs, uint32_t blk_lo,

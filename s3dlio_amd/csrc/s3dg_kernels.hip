@@ -2,24 +2,21 @@
 // generator.  Semantics: /root/reference/src/data_gen.rs:151-224
 // (fill_controlled_data), bit-exact for a given entropy and base block.
 //
-// Work decomposition (DESIGN.md §Kernels; measurements in profiles/):
-//   * ONE 256-thread workgroup per 4 KiB block, non-persistent grid in
-//     address order.  Each of the 4 waves writes one 1 KiB quarter with a
-//     single 16-byte store per lane (global_store_dwordx4).  Measured on
-//     MI355X this is the write pattern that reaches the HBM write ceiling
-//     (6.9-7.0 TB/s, = hipMemset-class fill): short-lived workgroups
-//     dispatched in order keep the write frontier compact, whereas
-//     persistent or multi-block workgroups stay at 5.0-6.3 TB/s.
+// Work decomposition (DESIGN.md §5; measurements in profiles/):
+//   * ONE workgroup per 4 KiB block, non-persistent grid in address order:
+//     2 waves per block for streams (each lane two 16-byte stores), 1 wave
+//     for batches (four).  Short-lived workgroups dispatched in order keep
+//     the write frontier compact; persistent or looping workgroups stayed at
+//     5.0-6.3 TB/s on MI355X.
+//   * Resident workgroups per CU are capped through reserved LDS (stream:
+//     12); fewer blocks in flight write HBM faster than the hardware maximum.
+//     Batch workgroups warm the L2 with a later tile record instead.
 //   * Wave 0 derives the block's parameters (u = i % U, zero-prefix length,
 //     window offsets) and runs the block's PRNG chain ONCE (SplitMix64 seed
-//     expansion + <= 8 Xoshiro256++ draws; wave-uniform, so it runs on the
-//     scalar unit), publishes them to LDS, then a workgroup barrier.  Running
-//     the chain in more than one wave per block made the kernel
-//     compute-bound (64-bit multiplies), see DESIGN.md.
-//   * Every lane then stores base-block bytes (16 B per lane, read once per
-//     workgroup from L2) or zeros; only the <= 6 lanes per block that straddle
-//     a window / the zero boundary / the object tail take the byte-masked
-//     slow path (LDS window image + v_alignbyte).  No HBM reads: dedup blocks
+//     words on the VALU, the 8 Xoshiro256++ steps on the scalar unit), then
+//     patches the zero bytes and the two 32-byte windows into an LDS image of
+//     the base block.  After a barrier every lane stores its 16-byte pieces
+//     (zeros below the prefix, the image above).  No HBM reads: dedup blocks
 //     are recomputed, never copied.
 #include "s3dg_internal.h"
 
@@ -286,19 +283,25 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t 
 
 // Batch: workgroup g -> tile record g/64 (one scalar load), block
 // first + (g % 64) of that object; blocks past the object's end exit.
+// pf > 0: the first 8 workgroups of a tile (one per XCD: workgroups are dealt
+// round-robin to the XCDs) load the record of tile + pf after their stores,
+// result unused, so it is in that XCD's L2 when its workgroups start.  pf must
+// exceed the tiles in flight (resident workgroups / 64); see DESIGN.md §5.1.
 template <bool NT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
-                                                        uint64_t g0, const u32x4 *base) {
+                                                        uint64_t ntiles, uint64_t g0, uint32_t pf,
+                                                        const u32x4 *base) {
     __shared__ __attribute__((aligned(16))) BlockLds S;
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t g = g0 + blockIdx.x;
+    const uint64_t tile = g >> 6;
     // The tile record (64 B) in ONE scalar load, issued first; then the base
     // block's vector loads and its LDS image, so the two memory latencies
     // overlap instead of following each other (the compiler otherwise splits
     // the record into four loads around the early-exit branch).
     u32x16 raw;
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + (g >> 6)) : "memory");
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + tile) : "memory");
     u32x4 B[4 / NW];
     load_base<NW>(B, t, base);
     store_image<NW>(S, t, B);
@@ -310,6 +313,12 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     if (ib * kBlk >= e.size) return;               // uniform for the whole workgroup
     gen_block<NT, NW, true>(dst_base + e.dst_off + (uint64_t)k * kBlk, S, t, wave, (uint32_t)ib, e.size,
                             e.entropy, e.pp, B);
+    if (pf && k < 8 && t == 0) {
+        const uint64_t pt = tile + pf;
+        const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
+        uint32_t dummy;
+        asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
+    }
 }
 
 // tiles[tile] = record of every 64-block tile of every object.
@@ -330,13 +339,16 @@ __global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t 
     }
 }
 
-// Write-only ceiling in the same shape (one 4 KiB chunk per 256-thread workgroup).
-template <bool NT>
-__global__ __launch_bounds__(256) void k_write_ceiling(uint8_t *dst, uint64_t nchunks, uint64_t g0,
-                                                       uint32_t pat) {
+// Write-only ceiling in the fill kernels' shape: one 4 KiB chunk per
+// (64*NW)-thread workgroup, 16-byte stores, same occupancy cap.
+template <bool NT, int NW>
+__global__ __launch_bounds__(64 * NW) void k_write_ceiling(uint8_t *dst, uint64_t nchunks, uint64_t g0,
+                                                           uint32_t pat) {
     const u32x4 v = {pat, pat ^ 0x9E3779B9u, pat + 1u, ~pat};
     const uint64_t g = g0 + blockIdx.x;
-    if (g < nchunks) store16<NT>(dst + g * kBlk + threadIdx.x * 16, v);
+    if (g >= nchunks) return;
+#pragma unroll
+    for (int k = 0; k < 4 / NW; ++k) store16<NT>(dst + g * kBlk + (threadIdx.x + k * 64 * NW) * 16, v);
 }
 
 
@@ -493,17 +505,23 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
 constexpr uint64_t kMaxGridX = 1ull << 22;
 
 template <bool NT, int NW>
-void launch_stream_one(dim3 g, hipStream_t s, uint8_t *d, uint64_t obj_size, uint64_t stride,
+void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t obj_size, uint64_t stride,
                        uint32_t blk_lo, uint64_t y0, uint64_t seed_base, uint64_t first_obj,
                        PrefixParams pp, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_stream<NT, NW>), g, dim3(64 * NW), 0, s, d, obj_size, stride, blk_lo,
+    hipLaunchKernelGGL((k_fill_stream<NT, NW>), g, dim3(64 * NW), lds, s, d, obj_size, stride, blk_lo,
                        y0, seed_base, first_obj, pp, b);
 }
 
 template <bool NT, int NW>
-void launch_batch_one(dim3 g, hipStream_t s, uint8_t *d, const TileRec *tiles, uint64_t g0,
-                      const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), 0, s, d, tiles, g0, b);
+void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
+                      uint64_t ntiles, uint64_t g0, uint32_t pf, const u32x4 *b) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, b);
+}
+
+template <bool NT, int NW>
+void launch_ceiling_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t nch, uint64_t g0,
+                        uint32_t pattern) {
+    hipLaunchKernelGGL((k_write_ceiling<NT, NW>), g, dim3(64 * NW), lds, s, d, nch, g0, pattern);
 }
 
 #define S3DG_DISPATCH(fn, lc, ...)                                              \
@@ -519,7 +537,44 @@ void launch_batch_one(dim3 g, hipStream_t s, uint8_t *d, const TileRec *tiles, u
         }                                                                       \
     } while (0)
 
+template <bool NT, int NW>
+hipError_t occ_one(bool batch, uint32_t lds, int *out) {
+    if (batch)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            out, reinterpret_cast<const void *>(&k_fill_batch<NT, NW>), 64 * NW, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        out, reinterpret_cast<const void *>(&k_fill_stream<NT, NW>), 64 * NW, lds);
+}
+
 }  // namespace
+
+#define S3DG_DISPATCH_RET(r, fn, lc, ...)                                       \
+    do {                                                                        \
+        if (lc.nontemporal) {                                                   \
+            if (lc.waves_per_block == 1) r = fn<true, 1>(__VA_ARGS__);          \
+            else if (lc.waves_per_block == 4) r = fn<true, 4>(__VA_ARGS__);     \
+            else r = fn<true, 2>(__VA_ARGS__);                                  \
+        } else {                                                                \
+            if (lc.waves_per_block == 1) r = fn<false, 1>(__VA_ARGS__);         \
+            else if (lc.waves_per_block == 4) r = fn<false, 4>(__VA_ARGS__);    \
+            else r = fn<false, 2>(__VA_ARGS__);                                 \
+        }                                                                       \
+    } while (0)
+
+uint32_t occupancy_lds(int wgs, uint32_t static_lds) {
+    if (wgs <= 0) return 0;
+    constexpr uint32_t kLdsPerCu = 160u * 1024u, kGranule = 512u;
+    // smallest granule-rounded footprint with floor(kLdsPerCu / footprint) == wgs
+    uint32_t total = (kLdsPerCu / (uint32_t)(wgs + 1)) / kGranule * kGranule + kGranule;
+    if (total < static_lds) return 0;
+    return total - static_lds;
+}
+
+hipError_t fill_occupancy(const LaunchCfg &lc, bool batch, int *wgs_per_cu) {
+    hipError_t e;
+    S3DG_DISPATCH_RET(e, occ_one, lc, batch, lc.dyn_lds, wgs_per_cu);
+    return e;
+}
 
 hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size,
                               uint64_t stride, uint64_t n_objs, uint32_t blk_lo,
@@ -532,7 +587,7 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
         const uint32_t ny = (uint32_t)((n_objs - y0) < 65535 ? (n_objs - y0) : 65535);
         for (uint64_t x0 = 0; x0 < nx; x0 += kMaxGridX) {
             const uint32_t gx = (uint32_t)((nx - x0) < kMaxGridX ? (nx - x0) : kMaxGridX);
-            S3DG_DISPATCH(launch_stream_one, lc, dim3(gx, ny), s, dst + x0 * kBlk, obj_size, stride,
+            S3DG_DISPATCH(launch_stream_one, lc, dim3(gx, ny), lc.dyn_lds, s, dst + x0 * kBlk, obj_size, stride,
                           (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -552,7 +607,8 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
     const uint64_t total = total_tiles * kTileBlocks;
     for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
-        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), s, dst_base, tiles, g0, b);
+        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
+                      lc.prefetch_tiles, b);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -575,10 +631,7 @@ hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
     const uint64_t nch = len / kBlk;
     for (uint64_t g0 = 0; g0 < nch; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((nch - g0) < kMaxGridX ? (nch - g0) : kMaxGridX);
-        if (lc.nontemporal)
-            hipLaunchKernelGGL(k_write_ceiling<true>, dim3(gx), dim3(256), 0, s, dst, nch, g0, pattern);
-        else
-            hipLaunchKernelGGL(k_write_ceiling<false>, dim3(gx), dim3(256), 0, s, dst, nch, g0, pattern);
+        S3DG_DISPATCH(launch_ceiling_one, lc, dim3(gx), lc.dyn_lds, s, dst, nch, g0, pattern);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

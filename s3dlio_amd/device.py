@@ -140,6 +140,21 @@ class Context:
     def set_nontemporal(self, on: bool) -> None:
         call("s3dg_set_nontemporal", self._h, 1 if on else 0)
 
+    def set_occupancy(self, stream_wgs_per_cu: int = -1, batch_wgs_per_cu: int = -1) -> None:
+        """Cap resident fill workgroups per CU (0 = hardware max, negative = library
+        default); results are identical."""
+        call("s3dg_set_occupancy", self._h, int(stream_wgs_per_cu), int(batch_wgs_per_cu))
+
+    def set_batch_prefetch(self, tiles: int) -> None:
+        """Tile-record prefetch distance of batch launches (0 = off); results are identical."""
+        call("s3dg_set_batch_prefetch", self._h, int(tiles))
+
+    def query_occupancy(self, batch: bool = False) -> int:
+        """Resident fill workgroups per CU under the current settings."""
+        out = ctypes.c_int()
+        call("s3dg_query_occupancy", self._h, 1 if batch else 0, ctypes.byref(out))
+        return out.value
+
     # -- generation (asynchronous on `stream`) ----------------------------------
     def fill_controlled(self, dst, nbytes: int | None = None, dedup: int = 1, compress=1,
                         entropy: int = 0, stream=None) -> None:

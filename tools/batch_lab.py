@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Diagnostic: fill-kernel launch-shape study on the product library.
+Sweeps the runtime knobs (waves per block, resident-workgroup cap per CU,
+batch tile-record prefetch distance) over cfg4 (log-uniform sizes, batch),
+cfg7 (uniform 8 MiB, batch) and cfg2 (uniform 8 MiB, stream), interleaved in
+one process, and prints GB/s per point.
+
+    python tools/batch_lab.py            # on the GPU box
+Tooling only: nothing in the product imports this."""
+import ctypes, itertools, json, os, statistics, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def points():
+    spec = os.environ.get("LAB_POINTS")
+    if spec:     # "kind:waves:occ:pf;..."
+        for p in spec.split(";"):
+            k, w, o, f = p.split(":")
+            yield k, int(w), int(o), int(f)
+        return
+    for w, o, f in itertools.product([1], [0, 28, 24, 20, 16], [0, 128]):
+        for k in ("cfg4", "cfg7"):
+            yield k, w, o, f
+    for w, o in [(2, 0), (2, 14), (2, 12)]:
+        for k in ("cfg4", "cfg7"):
+            yield k, w, o, 0
+    for w, o in [(2, 0), (2, 14), (2, 12), (1, 0), (1, 24), (1, 20), (1, 16)]:
+        yield "stream2", w, o, 0
+
+
+def main():
+    import torch
+    from bench import log_uniform_sizes, SEED_BASE
+    from s3dlio_amd import Context
+    from s3dlio_amd._lib import ObjDesc, call
+    MiB = 1 << 20
+    n = int(os.environ.get("LAB_N", "10000"))
+    ctx = Context(0)
+    descs = {}
+    for name, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3),
+                                   ("cfg7", [8 * MiB] * n, 1, 0, 1)]:
+        arr = (ObjDesc * n)()
+        off = 0
+        for j, sz in enumerate(sizes):
+            arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), d, fn, fd)
+            off += (sz + 4095) // 4096 * 4096
+        descs[name] = (arr, off, sum(sizes))
+    descs["stream2"] = (None, 8 * MiB * n, 8 * MiB * n)
+    descs["stream3"] = ("s3", 8 * MiB * n, 8 * MiB * n)        # cfg3: dedup 4, compress 2
+    descs["ceiling"] = ("c", 8 * MiB * n, 8 * MiB * n)         # store-only kernel, fill shapes
+    buf = torch.empty(max(v[1] for v in descs.values()), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    sh = int(st.cuda_stream)
+
+    def run(name):
+        arr = descs[name][0]
+        if name == "ceiling":
+            call("s3dg_write_ceiling", ctx._h, buf.data_ptr(), 8 * MiB * n, 0xA5A5A5A5, sh)
+            return
+        if arr is None or arr == "s3":
+            d, fn, fd = (1, 0, 1) if arr is None else (4, 1, 2)
+            call("s3dg_fill_controlled_stream", ctx._h, buf.data_ptr(), 8 * MiB, 8 * MiB, n, d, fn, fd,
+                 SEED_BASE, 0, sh)
+        else:
+            call("s3dg_fill_controlled_batch", ctx._h, buf.data_ptr(), arr, n, sh)
+
+    pts = list(points())
+    res, occ = {}, {}
+    for rep in range(int(os.environ.get("LAB_REPS", "3"))):
+        for p in pts:
+            k, w, o, f = p
+            ctx.set_waves_per_block(w)
+            ctx.set_occupancy(o, o)
+            ctx.set_batch_prefetch(f)
+            occ[p] = ctx.query_occupancy(batch=k.startswith("cfg"))
+            run(k)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st); run(k); e1.record(st); torch.cuda.synchronize()
+            res.setdefault(p, []).append(descs[k][2] / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+        print(f"rep {rep} done", flush=True)
+    for p, v in res.items():
+        k, w, o, f = p
+        print(json.dumps({"cfg": k, "waves": w, "occ_cap": o, "wgs_per_cu": occ[p], "pf": f,
+                          "GBps_median": round(statistics.median(v), 1), "max": round(max(v), 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
