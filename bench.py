@@ -170,7 +170,8 @@ def main() -> int:
     base_ptr = int(ring.data_ptr())
     batch = cfg["size"] is None
     if cfg.get("keystream"):
-        launch_shape = "one wave per 2 MiB chunk (64 lanes x 4096 draws, jump-ahead)"
+        launch_shape = ("k_keystream<64,4>: 128 lanes x 2048 draws per 2 MiB chunk (jump-ahead), "
+                        "64-draw LDS stage per lane, 512-B row pieces per store")
     else:
         waves = args.waves_per_block or (1 if batch else 2)
         launch_shape = (f"one {64 * waves}-thread workgroup per 4 KiB block, "

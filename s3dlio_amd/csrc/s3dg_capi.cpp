@@ -30,6 +30,10 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 using namespace s3dg;
 
 constexpr int kDefaultOccStream = 12, kDefaultOccBatch = 0;
+constexpr uint64_t kDefaultKsMinDraws = 2048;
+// measured on MI355X (tools/k2_lab.py): 512-B row pieces for the plain
+// keystream, 128-B pieces for DG1 (zero-prefixed 1 MiB blocks)
+constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0}, {16, 4, 0}};
 
 struct s3dg_ctx {
     int device = 0;
@@ -39,6 +43,9 @@ struct s3dg_ctx {
     // (DESIGN.md §5.1): 12 for 2-wave stream blocks, no cap for 1-wave batch blocks
     int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
     uint32_t prefetch_tiles = 128;     // batch tile-record prefetch distance
+    // k_keystream launch shapes, [0] npz keystream, [1] DG1
+    KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
+    uint64_t ks_min_draws[2] = {kDefaultKsMinDraws, kDefaultKsMinDraws};   // >= draws per lane
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // batch descriptor table (device) + pinned staging, grown on demand
@@ -248,6 +255,31 @@ int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
     return S3DG_OK;
 }
 
+int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wgs_per_cu,
+                             uint64_t min_lane_draws) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (mode != 0 && mode != 1) return fail(S3DG_EINVAL, "mode must be 0 (keystream) or 1 (dgen)");
+    if (draws != 0 && draws != 16 && draws != 32 && draws != 64)
+        return fail(S3DG_EINVAL, "draws per stage must be 16, 32 or 64");
+    if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(S3DG_EINVAL, "waves must be 1, 2 or 4");
+    if (wgs_per_cu < 0 || wgs_per_cu > 40) return fail(S3DG_EINVAL, "workgroups per CU must be 0..40");
+    if (min_lane_draws != 0 && min_lane_draws < 64) return fail(S3DG_EINVAL, "min_lane_draws must be >= 64");
+    std::lock_guard<std::mutex> g(c->mu);
+    const KsShape &def = kDefaultKsShape[mode];
+    c->ks[mode].draws = draws ? draws : def.draws;
+    c->ks[mode].waves = waves ? waves : def.waves;
+    c->ks[mode].wgs_per_cu = wgs_per_cu;
+    c->ks_min_draws[mode] = min_lane_draws ? min_lane_draws : kDefaultKsMinDraws;
+    return S3DG_OK;
+}
+
+int s3dg_query_keystream_occupancy(s3dg_ctx *c, int mode, int *wgs_per_cu) {
+    if (int r = check_ctx(c)) return r;
+    if (!wgs_per_cu || (mode != 0 && mode != 1)) return fail(S3DG_EINVAL, "bad argument");
+    HIP_TRY(keystream_occupancy(c->ks[mode], wgs_per_cu), "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    return S3DG_OK;
+}
+
 int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
     if (int r = check_ctx(c)) return r;
     if (!wgs_per_cu) return fail(S3DG_EINVAL, "null output");
@@ -412,20 +444,17 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
 }
 
 // lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
-static int keystream_plan(s3dg_ctx *c, uint64_t chunk_bytes, KeystreamArgs &A, const uint64_t **jtab) {
+static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, KeystreamArgs &A,
+                          const uint64_t **jtab) {
     const uint64_t nd = chunk_bytes / 8;
-    // as many lanes per chunk as keep >= min_draws draws per lane (the jump
-    // costs 256 steps); up to 1024 lanes = 16 waves per chunk.
-    // S3DLIO_K2_MIN_DRAWS overrides the default (tuning experiments).
-    static const uint64_t min_draws = [] {
-        const char *e = getenv("S3DLIO_K2_MIN_DRAWS");
-        const long v = e ? atol(e) : 0;
-        return v >= 64 ? (uint64_t)v : (uint64_t)2048;
-    }();
+    // as many lanes per chunk as keep >= ks_min_draws draws per lane (the
+    // jump costs 256 steps); up to 1024 lanes = 16 waves per chunk
+    const uint64_t min_draws = c->ks_min_draws[mode];
     uint32_t lpc = 1;
     while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
     uint64_t span = (nd + lpc - 1) / lpc;
-    span = (span + 15) / 16 * 16;
+    const uint64_t D = (uint64_t)c->ks[mode].draws;    // a lane stages D draws per iteration
+    span = (span + D - 1) / D * D;
     if (span > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "chunk too large");
     A.lpc = lpc;
     A.span = (uint32_t)span;
@@ -455,7 +484,7 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, chunk_bytes, A, &jt)) return r;
+    if (int r = keystream_plan(c, 0, chunk_bytes, A, &jt)) return r;
     A.nchunks = (len + chunk_bytes - 1) / chunk_bytes;
     A.chunk_bytes = chunk_bytes;
     A.obj_len = len;
@@ -466,7 +495,7 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
     A.m_unique = 0;
     A.zf_num = 0;
     A.zf_den = 1;
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, (hipStream_t)stream), "launch k_keystream");
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, c->ks[0], (hipStream_t)stream), "launch k_keystream");
     return S3DG_OK;
 }
 
@@ -497,7 +526,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, kDgenBlock, A, &jt)) return r;
+    if (int r = keystream_plan(c, 1, kDgenBlock, A, &jt)) return r;
     const uint64_t U = s3dg_unique_blocks(nb, dedup);
     A.cpo = blk_hi - blk_lo;
     A.nchunks = A.cpo * n_objs;
@@ -512,7 +541,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     A.m_unique = fastmod_magic(U == nb ? 1u : (uint32_t)U);
     A.zf_num = f_num;
     A.zf_den = f_den;
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, (hipStream_t)stream), "launch k_keystream(dgen)");
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, c->ks[1], (hipStream_t)stream), "launch k_keystream(dgen)");
     return S3DG_OK;
 }
 

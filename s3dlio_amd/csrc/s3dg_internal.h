@@ -90,8 +90,14 @@ struct KeystreamArgs {
     uint64_t cpo, obj_stride, seed_step;
 };
 
+// k_keystream launch shape: draws staged per lane per iteration (16, 32, 64),
+// waves per workgroup (1, 2, 4), resident workgroups per CU cap (0 = none).
+struct KsShape {
+    int draws, waves, wgs_per_cu;
+};
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
-                           hipStream_t s);
+                           const KsShape &sh, hipStream_t s);
+hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu);
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
                                 uint32_t pattern, hipStream_t s);

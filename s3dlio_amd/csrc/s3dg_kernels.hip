@@ -358,18 +358,23 @@ __global__ __launch_bounds__(64 * NW) void k_write_ceiling(uint8_t *dst, uint64_
 //   Xoshiro256PlusPlus::seed_from_u64(seed_base + c).fill_bytes(chunk).
 // `lpc` lanes share a chunk: lane `sub` starts at draw sub*span via the
 // jump polynomial jtab[sub] = x^(sub*span) mod P (s3dg_jump.cpp), 256 steps.
-// Each iteration a lane makes 16 draws (128 B) into its LDS row; the wave
-// then writes 8 rows' worth of whole 128-byte lines per store instruction
-// (8 lanes x 16 B per line), so every store covers full cache lines.
-constexpr int kRowStride = 144;   // 128 B + 16 B pad: conflict-light ds_write_b128 rows
-
+// Each iteration a lane makes D draws (8D bytes) into its LDS row; the wave
+// then writes the 64 rows out with 16-byte pieces, P = D/2 pieces per row and
+// 64/P rows per store instruction, so every store covers whole 8D-byte row
+// segments (D = 16: 128 B, 8 rows per instruction; D = 64: 512 B, 2 rows).
+// W waves per workgroup; LDS = W * 64 * (8D + 16) bytes.
 __device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2, uint64_t &s3) {
     const uint64_t t = s1 << 17;
     s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotlk<45>(s3);
 }
 
-__global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
-    __shared__ __attribute__((aligned(16))) uint8_t rows[4][64 * kRowStride];
+template <int D, int W>
+__global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
+    static_assert(D == 16 || D == 32 || D == 64, "draws per stage");
+    constexpr int RS = D * 8 + 16;     // row stride: + 16 B pad, conflict-light ds_write_b128 rows
+    constexpr int P = D / 2;           // 16-byte pieces per row
+    constexpr int R = 64 / P;          // rows per store instruction
+    __shared__ __attribute__((aligned(16))) uint8_t rows[W][64 * RS];
     const uint32_t t = threadIdx.x, l = t & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     uint8_t *myrows = rows[w];
@@ -377,7 +382,7 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
     // global lane gl -> chunk gl / lpc, lane-in-chunk gl % lpc (lpc: power of two;
     // lpc > 64 spreads one chunk over lpc/64 waves)
     const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
-    const uint64_t gl = ((uint64_t)blockIdx.x * 4 + w) * 64 + l;
+    const uint64_t gl = ((uint64_t)blockIdx.x * W + w) * 64 + l;
     const uint64_t c = gl >> lsh;                                    // local chunk index
     const uint64_t cpo = A.cpo ? A.cpo : A.nchunks;
     const uint64_t ko = c / cpo;                                     // object within the launch
@@ -421,42 +426,42 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
 
-    // destination of the 8 rows this lane helps write: row 8i + l/8, piece l%8
-    const uint32_t piece = l & 7;
-    uint64_t raddr[8];
-    uint32_t rrem[8];
+    // destination of the P rows this lane helps write: row R*i + l/P, piece l%P
+    const uint32_t piece = l % P;
+    uint64_t raddr[P];
+    uint32_t rrem[P];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t r = 8 * i + (l >> 3);
+    for (int i = 0; i < P; ++i) {
+        const uint32_t r = R * i + l / P;
         raddr[i] = __shfl(coff + rb, (int)r);
         rrem[i] = __shfl(rlen, (int)r);
     }
     const uint64_t d0 = (uint64_t)sub * span;                        // first draw index
-    const uint32_t iters = span / 16;
-    // Wave-uniform fast paths: a 16-draw group needs no masking when no lane
+    const uint32_t iters = span / D;
+    // Wave-uniform fast paths: a D-draw group needs no masking when no lane
     // of the wave is inside a zero prefix or at its chunk's 1-4 byte tail;
     // the stores need no guards when every region of the wave is full length.
     const bool full_rows = __all(rlen == span * 8u);
     // Per lane: iterations < it_plain may touch the zero prefix (draws below
     // ceil(zlen/8)); iteration it_tail holds the 1-4 byte tail draw.
     const uint64_t zdraws = (zlen + 7) >> 3;
-    const uint64_t zi = zdraws > d0 ? (zdraws - d0 + 15) / 16 : 0;
+    const uint64_t zi = zdraws > d0 ? (zdraws - d0 + D - 1) / D : 0;
     const uint32_t it_plain = zi < iters ? (uint32_t)zi : iters;
     const uint32_t it_tail = (tail_hi && tail_draw >= d0 && tail_draw < d0 + span)
-                                 ? (uint32_t)((tail_draw - d0) / 16) : 0xFFFFFFFFu;
+                                 ? (uint32_t)((tail_draw - d0) / D) : 0xFFFFFFFFu;
     for (uint32_t it = 0; it < iters; ++it) {
-        const uint64_t dg = d0 + (uint64_t)it * 16;
+        const uint64_t dg = d0 + (uint64_t)it * D;
         if (__all(it >= it_plain && it != it_tail)) {
 #pragma unroll
-            for (int q = 0; q < 16; q += 2) {
+            for (int q = 0; q < D; q += 2) {
                 const uint64_t ra = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
                 const uint64_t rbv = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
-                *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
+                *reinterpret_cast<u32x4 *>(myrows + l * RS + q * 8) =
                     u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < 16; q += 2) {
+            for (int q = 0; q < D; q += 2) {
                 uint64_t ra = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
                 uint64_t rbv = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
                 const uint64_t d = dg + q;
@@ -464,27 +469,27 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
                 if (tail_hi && d + 1 == tail_draw) rbv >>= 32;
                 if (8 * d < zlen) ra &= (8 * d + 8 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d)));
                 if (8 * d + 8 < zlen) rbv &= (8 * d + 16 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d - 8)));
-                *reinterpret_cast<u32x4 *>(myrows + l * kRowStride + q * 8) =
+                *reinterpret_cast<u32x4 *>(myrows + l * RS + q * 8) =
                     u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t o = it * 128 + piece * 16;                   // offset within the row's region
+        const uint32_t o = it * (D * 8) + piece * 16;               // offset within the row's region
         if (full_rows) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t r = 8 * i + (l >> 3);
+            for (int i = 0; i < P; ++i) {
+                const uint32_t r = R * i + l / P;
                 *reinterpret_cast<u32x4 *>(dst + raddr[i] + o) =
-                    *reinterpret_cast<const u32x4 *>(myrows + r * kRowStride + piece * 16);
+                    *reinterpret_cast<const u32x4 *>(myrows + r * RS + piece * 16);
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t r = 8 * i + (l >> 3);
+            for (int i = 0; i < P; ++i) {
+                const uint32_t r = R * i + l / P;
                 if (o >= rrem[i]) continue;
-                const u32x4 v = *reinterpret_cast<const u32x4 *>(myrows + r * kRowStride + piece * 16);
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(myrows + r * RS + piece * 16);
                 uint8_t *p = dst + raddr[i] + o;
                 if (o + 16 <= rrem[i]) {
                     *reinterpret_cast<u32x4 *>(p) = v;
@@ -499,6 +504,33 @@ __global__ __launch_bounds__(256) void k_keystream(uint8_t *dst, KeystreamArgs A
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
+
+template <int D, int W>
+hipError_t launch_ks_one(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab, uint32_t lds,
+                         hipStream_t s) {
+    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
+    const uint64_t wgs = (waves + W - 1) / W;
+    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_keystream<D, W>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+    return hipGetLastError();
+}
+
+template <int D, int W>
+hipError_t occ_ks_one(uint32_t lds, int *out) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        out, reinterpret_cast<const void *>(&k_keystream<D, W>), 64 * W, lds);
+}
+
+// static LDS of k_keystream<D, W>
+constexpr uint32_t ks_static_lds(int D, int W) { return (uint32_t)W * 64u * (uint32_t)(D * 8 + 16); }
+
+#define S3DG_KS_DISPATCH(r, fn, sh, ...)                                         \
+    do {                                                                         \
+        const int d_ = (sh).draws, w_ = (sh).waves;                              \
+        if (d_ == 64) r = (w_ == 1 ? fn<64, 1>(__VA_ARGS__) : w_ == 2 ? fn<64, 2>(__VA_ARGS__) : fn<64, 4>(__VA_ARGS__)); \
+        else if (d_ == 32) r = (w_ == 1 ? fn<32, 1>(__VA_ARGS__) : w_ == 2 ? fn<32, 2>(__VA_ARGS__) : fn<32, 4>(__VA_ARGS__)); \
+        else r = (w_ == 1 ? fn<16, 1>(__VA_ARGS__) : w_ == 2 ? fn<16, 2>(__VA_ARGS__) : fn<16, 4>(__VA_ARGS__)); \
+    } while (0)
 
 // Grid sizes are 32-bit WORK-ITEM counts in the AQL dispatch packet: cap a
 // launch at 2^22 workgroups per dimension (x 256 threads < 2^32).
@@ -616,13 +648,19 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
 }
 
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
-                           hipStream_t s) {
+                           const KsShape &sh, hipStream_t s) {
     (void)hipGetLastError();
-    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
-    const uint64_t wgs = (waves + 3) / 4;
-    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_keystream, dim3((uint32_t)wgs), dim3(256), 0, s, dst, A, jtab);
-    return hipGetLastError();
+    const uint32_t lds = occupancy_lds(sh.wgs_per_cu, ks_static_lds(sh.draws, sh.waves));
+    hipError_t e;
+    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, s);
+    return e;
+}
+
+hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu) {
+    const uint32_t lds = occupancy_lds(sh.wgs_per_cu, ks_static_lds(sh.draws, sh.waves));
+    hipError_t e;
+    S3DG_KS_DISPATCH(e, occ_ks_one, sh, lds, wgs_per_cu);
+    return e;
 }
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len, uint32_t pattern,

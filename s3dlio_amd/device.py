@@ -149,6 +149,18 @@ class Context:
         """Tile-record prefetch distance of batch launches (0 = off); results are identical."""
         call("s3dg_set_batch_prefetch", self._h, int(tiles))
 
+    def set_keystream_shape(self, mode: int, draws: int = 0, waves: int = 0, wgs_per_cu: int = 0,
+                            min_lane_draws: int = 0) -> None:
+        """k_keystream launch shape for mode 0 (npz keystream) or 1 (DG1);
+        0 = default for each; results are identical."""
+        call("s3dg_set_keystream_shape", self._h, int(mode), int(draws), int(waves), int(wgs_per_cu),
+             int(min_lane_draws))
+
+    def query_keystream_occupancy(self, mode: int = 0) -> int:
+        out = ctypes.c_int()
+        call("s3dg_query_keystream_occupancy", self._h, int(mode), ctypes.byref(out))
+        return out.value
+
     def query_occupancy(self, batch: bool = False) -> int:
         """Resident fill workgroups per CU under the current settings."""
         out = ctypes.c_int()

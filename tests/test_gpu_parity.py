@@ -281,6 +281,36 @@ def test_keystream_vs_oracle(gpu_ctx, torch, oracle, length, chunk, sb):
     assert (h[length:] == GUARD).all()
 
 
+KS_SHAPES = [(16, 4, 0, 0), (16, 1, 0, 0), (32, 2, 0, 0), (64, 4, 0, 0), (64, 1, 3, 0),
+             (64, 2, 0, 4096), (32, 4, 1, 64), (16, 2, 0, 128)]
+
+
+@pytest.mark.parametrize("shape", KS_SHAPES)
+def test_keystream_shapes_vs_oracle(gpu_ctx, torch, oracle, shape):
+    """Every k_keystream launch shape (stage depth, waves per workgroup,
+    occupancy cap, lanes per chunk) writes the same bytes, in both modes."""
+    gpu_ctx.set_keystream_shape(0, *shape)
+    gpu_ctx.set_keystream_shape(1, *shape)
+    try:
+        for length, chunk, sb in [(8 * 2**20 + 5, 2 * 2**20, 4), (2**20 + 6, 256 * 1024, 9),
+                                  (10 * 1152 + 3, 1152, 77)]:
+            t = torch.full((length + 64,), GUARD, dtype=torch.uint8, device="cuda")
+            gpu_ctx.xoshiro_fill(t, length, chunk_bytes=chunk, seed_base=sb)
+            h = t.cpu().numpy()
+            assert np.array_equal(h[:length], oracle.xoshiro_chunks(length, chunk, sb)), (shape, length)
+            assert (h[length:] == GUARD).all()
+        for size, d, c, seed in [(5 * 2**20 + 7, 2, 3, 5), (3 * 2**20, 1, 1, 11), (2**20 + 3, 1, 2, 2**64 - 1)]:
+            t = torch.full((size + 64,), GUARD, dtype=torch.uint8, device="cuda")
+            gpu_ctx.dgen_fill(t, size, dedup=d, compress=c, seed=seed)
+            h = t.cpu().numpy()
+            fn, fd = P.compress_ratio(c)
+            assert np.array_equal(h[:size], oracle.dgen_fill(size, d, fn, fd, seed)), (shape, size)
+            assert (h[size:] == GUARD).all()
+    finally:
+        gpu_ctx.set_keystream_shape(0)
+        gpu_ctx.set_keystream_shape(1)
+
+
 def test_keystream_full_size_properties(gpu_ctx, torch, oracle):
     """8 GiB of 2 MiB chunks: sampled chunks bit-exact, bytes ~uniform."""
     n = 8 * 2**30
