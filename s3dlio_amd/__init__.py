@@ -6,6 +6,7 @@ libs3dlio_amd.so).  Importing this package loads the library; it raises if
 the library is absent (no CPU fallback exists).
 """
 from ._lib import S3dgError, lib  # noqa: F401  (loads libs3dlio_amd.so)
+from .hostbuf import BytesView  # noqa: F401
 from .device import (BLOCK_SIZE, DEFAULT_BASE_SEED, Context, compress_ratio,  # noqa: F401
                      device_count, object_entropy, unique_blocks, xoshiro_jump)
 from .data_gen import fill_controlled_data, fill_controlled_data_seeded  # noqa: F401

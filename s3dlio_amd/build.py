@@ -34,7 +34,30 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
 
 
+BV_SRC = os.path.join(CSRC, "bytesview.c")
+
+
+def _bytesview_path() -> str:
+    import sysconfig
+    return os.path.join(PKG, "_bytesview" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_bytesview(force: bool = False, verbose: bool = False) -> str:
+    """The BytesView CPython extension type (gcc against this interpreter's headers)."""
+    import sysconfig
+    out = _bytesview_path()
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(BV_SRC):
+        return out
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Werror",
+           "-I", sysconfig.get_paths()["include"], "-o", out, BV_SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    build_bytesview(force, verbose)
     if not force and not _stale():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",

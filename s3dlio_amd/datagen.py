@@ -85,7 +85,7 @@ class _Gen:
             pass
 
 
-def _new_bytes(size: int, dedup: int, compress, seed: int | None) -> memoryview:
+def _new_bytes(size: int, dedup: int, compress, seed: int | None):
     out = hostbuf.empty(size)                # every byte is written by the generator
     if size:
         g = _Gen(size, dedup, compress, seed)
@@ -295,23 +295,23 @@ class GeneratorConfig:
 class DataBuffer:
     """dgen_data::DataBuffer: owned generated bytes (.into_bytes(), .as_slice(), .as_ptr())."""
 
-    def __init__(self, view: memoryview):
-        self._v = view
+    def __init__(self, view):
+        self._v = view            # BytesView
 
-    def into_bytes(self) -> memoryview:
+    def into_bytes(self):
         return self._v
 
     def as_slice(self) -> memoryview:
-        return self._v
+        return self._v.memoryview()
 
     def as_ptr(self) -> int:
-        return int(np.frombuffer(self._v, np.uint8).ctypes.data) if self._v.nbytes else 0
+        return int(np.frombuffer(self._v, np.uint8).ctypes.data) if len(self._v) else 0
 
     def __len__(self) -> int:
-        return self._v.nbytes
+        return len(self._v)
 
     def __bytes__(self) -> bytes:
-        return self._v.tobytes()
+        return self._v.to_bytes()
 
 
 def generate_data_from_config(config: GeneratorConfig) -> DataBuffer:
@@ -327,8 +327,8 @@ def generate_data_simple(size: int, dedup: int, compress: int) -> DataBuffer:
     return generate_data_from_config(GeneratorConfig(size, dedup, compress))
 
 
-def generate_data_with_config(config: GeneratorConfig) -> memoryview:
-    """src/data_gen_alt.rs:56-59 (Bytes = read-only zero-copy view)."""
+def generate_data_with_config(config: GeneratorConfig):
+    """src/data_gen_alt.rs:56-59 (Bytes = read-only zero-copy BytesView)."""
     return generate_data_from_config(config).into_bytes()
 
 

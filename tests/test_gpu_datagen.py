@@ -174,8 +174,10 @@ def test_generate_into_buffer_and_bytesview(S):
     """CI smoke (.github/workflows/ci.yml): generate_data(1024), memoryview,
     generate_into_buffer(bytearray(1024)); BytesView is read-only."""
     v = S.generate_data(1024)
+    assert isinstance(v, S.BytesView) and len(v) == 1024 and repr(v) == "BytesView(1024 bytes)"
     mv = memoryview(v)
     assert len(mv) == 1024 and mv.readonly
+    assert v.to_bytes() == bytes(v) == mv.tobytes() == bytes(v.memoryview())
     with pytest.raises((BufferError, TypeError)):
         mv[0] = 1
     b = bytearray(1024)

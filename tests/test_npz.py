@@ -46,7 +46,7 @@ def test_gpu_npz_byte_identical(shape, dtype, ns):
     """unet3d-style 140 MiB archive included (python_datagen_api.rs:389)."""
     import s3dlio_amd as S
     got = S.generate_npz_bytes(shape, dtype, ns)
-    assert got.readonly
+    assert memoryview(got).readonly and isinstance(got, S.BytesView)
     assert bytes(got) == N.generate_npz_bytes_raw(shape, dtype, ns)
 
 
