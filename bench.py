@@ -277,6 +277,8 @@ def main() -> int:
     d2h = None
     if not args.no_d2h and cfg["size"] is not None:
         d2h = d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo)
+        # every rank measures at the same time: the aggregate is what the node moves
+        d2h["aggregate_all_ranks"] = round(cp.sum(d2h["value"]), 2)
 
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
@@ -335,15 +337,23 @@ def traffic_from_profiles(config: int, launch_bytes: int):
     return None
 
 
-def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=512, per_chunk=32):
+def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=1024, per_chunk=32):
     """Generate n_objs objects through two device chunk buffers and copy each
-    chunk to a pinned host ring on a second stream (the PUT path's input)."""
+    chunk to a pinned host ring on the GPU's NUMA node, on a second stream
+    (the PUT path's input)."""
+    import ctypes
     size = cfg["size"]
     cb = per_chunk * size
     gen = torch.cuda.Stream(device=dev)
     cpy = torch.cuda.Stream(device=dev)
     devbuf = [torch.empty(cb, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(2)]
-    host = [torch.empty(cb, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    host = []
+    for _ in range(2):
+        p = ctypes.c_void_p()
+        call("s3dg_host_alloc_pinned_local", dev, cb, ctypes.byref(p))
+        host.append(p.value)
+    node = ctypes.c_int(-1)
+    call("s3dg_device_numa_node", dev, ctypes.byref(node))
     gen_done = [torch.cuda.Event() for _ in range(2)]
     cpy_done = [torch.cuda.Event() for _ in range(2)]
 
@@ -356,20 +366,24 @@ def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=512, per_c
                  int(gen.cuda_stream))
             gen_done[s].record(gen)
             cpy.wait_event(gen_done[s])
-            call("s3dg_d2h_async", ctx._h, int(host[s].data_ptr()), int(devbuf[s].data_ptr()),
-                 cb, int(cpy.cuda_stream))
+            call("s3dg_d2h_async", ctx._h, host[s], int(devbuf[s].data_ptr()), cb, int(cpy.cuda_stream))
             cpy_done[s].record(cpy)
-    for s in range(2):
-        cpy_done[s].record(cpy)
-    run(2 * per_chunk)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(n_objs)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    try:
+        for s in range(2):
+            cpy_done[s].record(cpy)
+        run(n_objs // 2)          # the first GiBs into fresh pinned pages copy slower
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(n_objs)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        torch.cuda.synchronize()
+        for p in host:
+            call("s3dg_host_free_pinned", p)
     return {"value": round(n_objs * size / dt / GiB, 2), "unit": "GiB/s",
             "sample": f"{n_objs} x {size // MiB} MiB objects, 2 x {per_chunk}-object device chunks, "
-                      "pinned host ring, generate || D2H on two streams"}
+                      f"pinned host ring on NUMA node {node.value}, generate || D2H on two streams"}
 
 
 def cpu_baseline(cfg, fn, fd, seconds):

@@ -145,7 +145,13 @@ int s3dg_write_ceiling(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern,
 int s3dg_device_alloc(s3dg_ctx *ctx, uint64_t bytes, void **out);
 int s3dg_device_free(s3dg_ctx *ctx, void *p);
 int s3dg_host_alloc_pinned(uint64_t bytes, void **out);
+/* Pinned host memory placed on `device`'s NUMA node (allocated from a thread
+ * bound to the GPU's local CPUs; falls back to default placement when sysfs
+ * does not say).  Free with s3dg_host_free_pinned. */
+int s3dg_host_alloc_pinned_local(int device, uint64_t bytes, void **out);
 int s3dg_host_free_pinned(void *p);
+/* NUMA node of `device` from sysfs (-1 when unknown). */
+int s3dg_device_numa_node(int device, int *node);
 int s3dg_d2h_async(s3dg_ctx *ctx, void *host, const void *dev, uint64_t len, void *stream);
 int s3dg_h2d_async(s3dg_ctx *ctx, void *dev, const void *host, uint64_t len, void *stream);
 int s3dg_stream_create(s3dg_ctx *ctx, void **out);

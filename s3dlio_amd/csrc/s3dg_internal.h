@@ -1,7 +1,10 @@
 // s3dg_internal.h — shared between the HIP kernels and the C-ABI layer.
 #pragma once
+#include <sched.h>
 #include <stdint.h>
 #include <hip/hip_runtime.h>
+
+extern "C" int s3dg_internal_fail(int code, const char *msg);
 
 namespace s3dg {
 
@@ -120,5 +123,21 @@ hipError_t crc_seg_launch(const CrcSegPlan &P, const uint8_t *dev, void *tab_dev
                           hipStream_t s);
 void crc_seg_fold(const CrcSegPlan &P, const uint32_t *regions, const uint8_t *const *tails,
                   uint32_t *crcs);
+
+// ---- NUMA placement of host buffers (s3dg_numa.cpp) -------------------------
+bool device_local_cpus(int device, cpu_set_t *out);
+int device_numa_node(int device);   // -1 when unknown
+// Binds the calling thread to the device's local CPUs for its lifetime (no-op
+// when sysfs has no answer or the affinity mask already lies inside them).
+class NumaScope {
+public:
+    explicit NumaScope(int device);
+    ~NumaScope();
+    NumaScope(const NumaScope &) = delete;
+    NumaScope &operator=(const NumaScope &) = delete;
+private:
+    cpu_set_t saved_;
+    bool active_ = false;
+};
 
 }  // namespace s3dg

@@ -44,7 +44,6 @@
 #include <thread>
 #include <vector>
 
-extern "C" int s3dg_internal_fail(int code, const char *msg);
 extern "C" int s3dg_internal_ctx_device(s3dg_ctx *c, int *dev);
 extern "C" int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride,
                                         uint64_t n_objs, uint64_t blk_lo, uint64_t blk_hi, uint64_t dedup,
@@ -104,6 +103,7 @@ int pool_init(PutPool &P, int device) {
         PUT_HIP(hipMalloc(&P.dev_reg[k], kMaxRegions * 4), "hipMalloc(put crc regions)");
         PUT_HIP(hipStreamCreateWithFlags(&P.st[k], hipStreamNonBlocking), "hipStreamCreate");
     }
+    NumaScope numa(device);            // the pinned ring on the GPU's NUMA node
     for (int k = 0; k < kHostSlots; ++k) {
         PUT_HIP(hipHostMalloc((void **)&P.host[k], kSlotBytes, hipHostMallocDefault), "hipHostMalloc(put ring)");
         PUT_HIP(hipHostMalloc((void **)&P.host_reg[k], kMaxRegions * 4, hipHostMallocDefault),

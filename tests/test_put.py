@@ -173,3 +173,31 @@ def test_gpu_put_io_error_is_loud(S, gpu_ctx, tmp_path):
     blocker.write_bytes(b"x")
     with pytest.raises(OSError):
         S.put_objects([f"file://{blocker}/under-a-file"], 4096, seed=1, context=gpu_ctx)
+
+
+@pytest.mark.gpu
+def test_numa_local_pinned_alloc_roundtrip():
+    """s3dg_host_alloc_pinned_local: pinned memory on the GPU's NUMA node,
+    usable as a D2H target."""
+    import ctypes
+    import numpy as np
+    import torch
+    import s3dlio_amd as S
+    from s3dlio_amd._lib import call
+    node = ctypes.c_int(-2)
+    call("s3dg_device_numa_node", 0, ctypes.byref(node))
+    assert node.value >= -1
+    ctx = S.Context(0)
+    n = 8 << 20
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.fill_controlled(dev, n, dedup=1, compress=1, entropy=3)
+    p = ctypes.c_void_p()
+    call("s3dg_host_alloc_pinned_local", 0, n, ctypes.byref(p))
+    try:
+        call("s3dg_d2h_async", ctx._h, p.value, dev.data_ptr(), n, 0)
+        call("s3dg_sync", ctx._h, 0)
+        host = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p.value))
+        assert np.array_equal(host, dev.cpu().numpy())
+    finally:
+        call("s3dg_host_free_pinned", p.value)
+        ctx.close()
