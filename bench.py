@@ -77,9 +77,10 @@ def parse():
     p.add_argument("--ring-gib", type=float, default=80.0,
                    help="device output ring per GPU (objects wrap when the step exceeds it)")
     p.add_argument("--waves-per-block", type=int, default=None, help="1, 2 or 4 (default 2)")
-    p.add_argument("--nt-stores", action="store_true", help="nontemporal stores (default plain)")
+    p.add_argument("--store", choices=["default", "plain", "nt", "sc1"], default="default",
+                   help="fill-kernel store cache policy (default: library's, sc1)")
     p.add_argument("--occupancy", type=int, default=None,
-                   help="resident fill workgroups per CU cap (default: library's, 12 stream / none batch)")
+                   help="resident fill workgroups per CU cap (default: library's, 14 stream / none batch)")
     p.add_argument("--prefetch", type=int, default=None,
                    help="batch tile-record prefetch distance in tiles (default: library's, 128)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -107,8 +108,9 @@ def main() -> int:
     dev = cp.local_rank if args.device_override is None else args.device_override
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
-    ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block,
-                  nontemporal=args.nt_stores)
+    ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block)
+    store = {"default": -1, "plain": 0, "nt": 1, "sc1": 2}[args.store]
+    ctx.set_store_policy(store, store)
     if args.occupancy is not None:
         ctx.set_occupancy(args.occupancy, args.occupancy)
     if args.prefetch is not None:
@@ -263,11 +265,14 @@ def main() -> int:
         torch.cuda.synchronize()
         return 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
     ceil_shapes = {}
-    for waves, occ in [(args.waves_per_block or 2, -1 if args.occupancy is None else args.occupancy),
-                       (4, 0), (4, 4), (4, 3), (2, 4)]:
+    names = {-1: "default", 0: "plain", 1: "nt", 2: "sc1"}
+    for waves, occ, sp in [(args.waves_per_block or 2, -1 if args.occupancy is None else args.occupancy, store),
+                           (4, 4, 2), (4, 3, 2), (2, 4, 2), (4, 0, 0), (4, 4, 0)]:
         ctx.set_waves_per_block(waves)
         ctx.set_occupancy(occ, occ)
-        ceil_shapes[f"{waves}w_{ctx.query_occupancy()}perCU"] = round(ceiling_rate(), 1)
+        ctx.set_store_policy(sp, sp)
+        ceil_shapes[f"{waves}w_{ctx.query_occupancy()}perCU_{names[sp]}"] = round(ceiling_rate(), 1)
+    ctx.set_store_policy(store, store)
     ceiling_gbs = max(ceil_shapes.values())
     ctx.set_waves_per_block(args.waves_per_block or 0)
     occ = -1 if args.occupancy is None else args.occupancy
@@ -303,7 +308,7 @@ def main() -> int:
                        "bytes_per_step_all_ranks": int(total_bytes // args.steps),
                        "dedup": cfg["dedup"], "compress": list(cfg["compress"]) if isinstance(cfg["compress"], tuple) else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
-                       "stores": "nontemporal" if args.nt_stores else "plain"},
+                       "stores": args.store if args.store != "default" else "sc1"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic_from_profiles(args.config, int(sum(launch_bytes) / len(launch_bytes))),

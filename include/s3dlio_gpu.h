@@ -67,11 +67,15 @@ int s3dg_get_base_block(s3dg_ctx *ctx, uint8_t *out4096);
 /* Wave64s per 4 KiB block = workgroup size / 64: 1, 2 or 4; 0 = auto
  * (2 for streams, 1 for batches).  A tuning knob; results are identical. */
 int s3dg_set_waves_per_block(s3dg_ctx *ctx, int waves);
-/* 1 = nontemporal stores, 0 = plain stores (default). */
+/* 1 = nontemporal stores in every fill kernel, 0 = the default policies. */
 int s3dg_set_nontemporal(s3dg_ctx *ctx, int on);
+/* Cache policy of the fill kernels' 16-byte stores, for stream and batch
+ * launches: 0 = plain, 1 = nt, 2 = sc1, negative = default (sc1 for both,
+ * measured on MI355X).  Results are identical. */
+int s3dg_set_store_policy(s3dg_ctx *ctx, int stream_policy, int batch_policy);
 /* Cap on resident fill workgroups per CU (reserved LDS), for stream and
  * batch launches separately; 0 = hardware maximum, negative = the default.
- * Defaults 12 (stream) and 0 (batch), measured on MI355X.  A tuning knob; results are identical. */
+ * Defaults 14 (stream) and 0 (batch), measured on MI355X.  A tuning knob; results are identical. */
 int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_cu);
 /* Batch launches: distance (in 64-block tiles) at which workgroups warm the
  * L2 with a later tile record; 0 = off.  Default 128.  Results are identical. */

@@ -54,6 +54,7 @@ SIGNATURES = {
     "s3dg_get_base_block": (c_int, [c_vp, c_u8p]),
     "s3dg_set_waves_per_block": (c_int, [c_vp, c_int]),
     "s3dg_set_nontemporal": (c_int, [c_vp, c_int]),
+    "s3dg_set_store_policy": (c_int, [c_vp, c_int, c_int]),
     "s3dg_set_occupancy": (c_int, [c_vp, c_int, c_int]),
     "s3dg_set_batch_prefetch": (c_int, [c_vp, c_u32]),
     "s3dg_query_occupancy": (c_int, [c_vp, c_int, ctypes.POINTER(c_int)]),

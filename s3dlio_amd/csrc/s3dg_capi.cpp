@@ -29,7 +29,8 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 
 using namespace s3dg;
 
-constexpr int kDefaultOccStream = 12, kDefaultOccBatch = 0;
+constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
+constexpr int kDefaultStoreStream = kStoreSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr uint64_t kDefaultKsMinDraws = 2048;
 // measured on MI355X (tools/k2_lab.py): 512-B row pieces for the plain
 // keystream, 128-B pieces for DG1 (zero-prefixed 1 MiB blocks)
@@ -37,10 +38,11 @@ constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0}, {16, 4, 0}};
 
 struct s3dg_ctx {
     int device = 0;
-    bool nontemporal = false;          // plain stores measured faster
+    // store cache policy: sc1 (write, then drop the line from L2) measured best
+    int store_stream = kDefaultStoreStream, store_batch = kDefaultStoreBatch;
     int waves_per_block = 0;           // 0 = auto: 2 for streams, 1 for batches (measured)
     // resident fill workgroups per CU (0 = hardware max); measured on MI355X
-    // (DESIGN.md §5.1): 12 for 2-wave stream blocks, no cap for 1-wave batch blocks
+    // (DESIGN.md §5.1): 14 for 2-wave stream blocks, no cap for 1-wave batch blocks
     int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
     uint32_t prefetch_tiles = 128;     // batch tile-record prefetch distance
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
@@ -129,7 +131,7 @@ int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den
 
 LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false) {
     LaunchCfg lc;
-    lc.nontemporal = c->nontemporal;
+    lc.store = batch ? c->store_batch : c->store_stream;
     lc.waves_per_block = c->waves_per_block ? c->waves_per_block : (batch ? 1 : 2);
     lc.dyn_lds = occupancy_lds(batch ? c->occ_batch : c->occ_stream, kFillStaticLds);
     lc.prefetch_tiles = batch ? c->prefetch_tiles : 0;
@@ -236,7 +238,17 @@ int s3dg_set_waves_per_block(s3dg_ctx *c, int waves) {
 
 int s3dg_set_nontemporal(s3dg_ctx *c, int on) {
     if (!c) return fail(S3DG_EINVAL, "null context");
-    c->nontemporal = on != 0;
+    c->store_stream = on ? kStoreNT : kDefaultStoreStream;
+    c->store_batch = on ? kStoreNT : kDefaultStoreBatch;
+    return S3DG_OK;
+}
+
+int s3dg_set_store_policy(s3dg_ctx *c, int stream_policy, int batch_policy) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (stream_policy > kStoreSC1 || batch_policy > kStoreSC1)
+        return fail(S3DG_EINVAL, "store policy must be 0 (plain), 1 (nt), 2 (sc1) or negative (default)");
+    c->store_stream = stream_policy < 0 ? kDefaultStoreStream : stream_policy;
+    c->store_batch = batch_policy < 0 ? kDefaultStoreBatch : batch_policy;
     return S3DG_OK;
 }
 

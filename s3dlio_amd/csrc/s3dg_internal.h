@@ -52,8 +52,11 @@ struct TileRec {
 };
 static_assert(sizeof(TileRec) == 64, "TileRec is one s_load_dwordx16");
 
+// store cache policy of the fill kernels (s3dg_set_store_policy)
+constexpr int kStorePlain = 0, kStoreNT = 1, kStoreSC1 = 2;
+
 struct LaunchCfg {
-    bool nontemporal;
+    int store;             // kStorePlain / kStoreNT / kStoreSC1
     int waves_per_block;   // 1, 2 or 4 wave64s per 4 KiB block (one workgroup)
     uint32_t dyn_lds = 0;  // reserved dynamic LDS per workgroup (occupancy cap)
     uint32_t prefetch_tiles = 0;   // batch: tile-record prefetch distance (0 = off)

@@ -9,8 +9,10 @@
 //     the write frontier compact; persistent or looping workgroups stayed at
 //     5.0-6.3 TB/s on MI355X.
 //   * Resident workgroups per CU are capped through reserved LDS (stream:
-//     12); fewer blocks in flight write HBM faster than the hardware maximum.
+//     14); fewer blocks in flight write HBM faster than the hardware maximum.
 //     Batch workgroups warm the L2 with a later tile record instead.
+//   * Stores are global_store_dwordx4 ... sc1: the line leaves the XCD's L2
+//     once written (plain stores keep it), measured 2-4 % faster.
 //   * Wave 0 derives the block's parameters (u = i % U, zero-prefix length,
 //     window offsets) and runs the block's PRNG chain ONCE (SplitMix64 seed
 //     words on the VALU, the 8 Xoshiro256++ steps on the scalar unit), then
@@ -74,9 +76,15 @@ struct Xoshiro {
     }
 };
 
-template <bool NT>
+// 16-byte store with a cache policy (LaunchCfg::store; tools/store_lab.py):
+//   kStorePlain  global_store_dwordx4 (line kept in the XCD's L2)
+//   kStoreNT     ... nt  (__builtin_nontemporal_store)
+//   kStoreSC1    ... sc1 (line dropped from the L2 once written)
+template <int SP>
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    if constexpr (SP == kStoreNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else if constexpr (SP == kStoreSC1)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
@@ -206,7 +214,7 @@ __device__ __forceinline__ void patch_image(BlockLds &S, const Plan &P, uint32_t
 }
 
 // Every lane, phase 3: its 16 bytes at byte o of the block: zeros below c, else the image.
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void write_block(uint8_t *bd, const BlockLds &S, int o) {
     const int c = (int)S.meta[0], L = (int)S.meta[1];
     if (o >= L) return;
@@ -240,7 +248,7 @@ __device__ __forceinline__ void store_image(BlockLds &S, uint32_t t, const u32x4
 }
 
 // IMG: the caller has already written the base image into S (batch kernel).
-template <bool NT, int NW, bool IMG = false>
+template <int NT, int NW, bool IMG = false>
 __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, uint32_t wave,
                                           uint32_t i, uint64_t size, uint64_t entropy,
                                           const PrefixParams &pp, const u32x4 (&B)[4 / NW]) {
@@ -262,7 +270,7 @@ __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, 
 }
 
 // Stream: blockIdx.x = block (blk_lo + x) of object (y0 + blockIdx.y).
-template <bool NT, int NW>
+template <int NT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t obj_size,
                                                      uint64_t stride, uint32_t blk_lo,
                                                      uint64_t y0, uint64_t seed_base,
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t 
 // round-robin to the XCDs) load the record of tile + pf after their stores,
 // result unused, so it is in that XCD's L2 when its workgroups start.  pf must
 // exceed the tiles in flight (resident workgroups / 64); see DESIGN.md §5.1.
-template <bool NT, int NW>
+template <int NT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
                                                         const u32x4 *base) {
@@ -341,7 +349,7 @@ __global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t 
 
 // Write-only ceiling in the fill kernels' shape: one 4 KiB chunk per
 // (64*NW)-thread workgroup, 16-byte stores, same occupancy cap.
-template <bool NT, int NW>
+template <int NT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_write_ceiling(uint8_t *dst, uint64_t nchunks, uint64_t g0,
                                                            uint32_t pat) {
     const u32x4 v = {pat, pat ^ 0x9E3779B9u, pat + 1u, ~pat};
@@ -536,7 +544,7 @@ constexpr uint32_t ks_static_lds(int D, int W) { return (uint32_t)W * 64u * (uin
 // launch at 2^22 workgroups per dimension (x 256 threads < 2^32).
 constexpr uint64_t kMaxGridX = 1ull << 22;
 
-template <bool NT, int NW>
+template <int NT, int NW>
 void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t obj_size, uint64_t stride,
                        uint32_t blk_lo, uint64_t y0, uint64_t seed_base, uint64_t first_obj,
                        PrefixParams pp, const u32x4 *b) {
@@ -544,32 +552,32 @@ void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t
                        y0, seed_base, first_obj, pp, b);
 }
 
-template <bool NT, int NW>
+template <int NT, int NW>
 void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
                       uint64_t ntiles, uint64_t g0, uint32_t pf, const u32x4 *b) {
     hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, b);
 }
 
-template <bool NT, int NW>
+template <int NT, int NW>
 void launch_ceiling_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t nch, uint64_t g0,
                         uint32_t pattern) {
     hipLaunchKernelGGL((k_write_ceiling<NT, NW>), g, dim3(64 * NW), lds, s, d, nch, g0, pattern);
 }
 
+#define S3DG_DISPATCH_W(SP, fn, lc, ...)                                        \
+    do {                                                                        \
+        if (lc.waves_per_block == 1) fn<SP, 1>(__VA_ARGS__);                    \
+        else if (lc.waves_per_block == 4) fn<SP, 4>(__VA_ARGS__);               \
+        else fn<SP, 2>(__VA_ARGS__);                                            \
+    } while (0)
 #define S3DG_DISPATCH(fn, lc, ...)                                              \
     do {                                                                        \
-        if (lc.nontemporal) {                                                   \
-            if (lc.waves_per_block == 1) fn<true, 1>(__VA_ARGS__);              \
-            else if (lc.waves_per_block == 4) fn<true, 4>(__VA_ARGS__);         \
-            else fn<true, 2>(__VA_ARGS__);                                      \
-        } else {                                                                \
-            if (lc.waves_per_block == 1) fn<false, 1>(__VA_ARGS__);             \
-            else if (lc.waves_per_block == 4) fn<false, 4>(__VA_ARGS__);        \
-            else fn<false, 2>(__VA_ARGS__);                                     \
-        }                                                                       \
+        if (lc.store == kStoreNT) S3DG_DISPATCH_W(kStoreNT, fn, lc, __VA_ARGS__);    \
+        else if (lc.store == kStoreSC1) S3DG_DISPATCH_W(kStoreSC1, fn, lc, __VA_ARGS__); \
+        else S3DG_DISPATCH_W(kStorePlain, fn, lc, __VA_ARGS__);                \
     } while (0)
 
-template <bool NT, int NW>
+template <int NT, int NW>
 hipError_t occ_one(bool batch, uint32_t lds, int *out) {
     if (batch)
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -580,17 +588,17 @@ hipError_t occ_one(bool batch, uint32_t lds, int *out) {
 
 }  // namespace
 
+#define S3DG_DISPATCH_RET_W(r, SP, fn, lc, ...)                                 \
+    do {                                                                        \
+        if (lc.waves_per_block == 1) r = fn<SP, 1>(__VA_ARGS__);                \
+        else if (lc.waves_per_block == 4) r = fn<SP, 4>(__VA_ARGS__);           \
+        else r = fn<SP, 2>(__VA_ARGS__);                                        \
+    } while (0)
 #define S3DG_DISPATCH_RET(r, fn, lc, ...)                                       \
     do {                                                                        \
-        if (lc.nontemporal) {                                                   \
-            if (lc.waves_per_block == 1) r = fn<true, 1>(__VA_ARGS__);          \
-            else if (lc.waves_per_block == 4) r = fn<true, 4>(__VA_ARGS__);     \
-            else r = fn<true, 2>(__VA_ARGS__);                                  \
-        } else {                                                                \
-            if (lc.waves_per_block == 1) r = fn<false, 1>(__VA_ARGS__);         \
-            else if (lc.waves_per_block == 4) r = fn<false, 4>(__VA_ARGS__);    \
-            else r = fn<false, 2>(__VA_ARGS__);                                 \
-        }                                                                       \
+        if (lc.store == kStoreNT) S3DG_DISPATCH_RET_W(r, kStoreNT, fn, lc, __VA_ARGS__);    \
+        else if (lc.store == kStoreSC1) S3DG_DISPATCH_RET_W(r, kStoreSC1, fn, lc, __VA_ARGS__); \
+        else S3DG_DISPATCH_RET_W(r, kStorePlain, fn, lc, __VA_ARGS__);         \
     } while (0)
 
 uint32_t occupancy_lds(int wgs, uint32_t static_lds) {

@@ -101,7 +101,8 @@ class Context:
             call("s3dg_set_base_block_seed", self._h, int(base_seed))
         if waves_per_block is not None:
             call("s3dg_set_waves_per_block", self._h, int(waves_per_block))
-        call("s3dg_set_nontemporal", self._h, 1 if nontemporal else 0)
+        if nontemporal:
+            call("s3dg_set_nontemporal", self._h, 1)
 
     # -- lifecycle -------------------------------------------------------------
     def close(self) -> None:
@@ -139,6 +140,10 @@ class Context:
 
     def set_nontemporal(self, on: bool) -> None:
         call("s3dg_set_nontemporal", self._h, 1 if on else 0)
+
+    def set_store_policy(self, stream_policy: int = -1, batch_policy: int = -1) -> None:
+        """Fill-kernel store cache policy: 0 plain, 1 nt, 2 sc1, -1 default; results are identical."""
+        call("s3dg_set_store_policy", self._h, int(stream_policy), int(batch_policy))
 
     def set_occupancy(self, stream_wgs_per_cu: int = -1, batch_wgs_per_cu: int = -1) -> None:
         """Cap resident fill workgroups per CU (0 = hardware max, negative = library

@@ -103,12 +103,13 @@ def test_stream_vs_oracle(gpu_ctx, torch, oracle, base, size, stride, n, d, c, f
     assert (got[stride * n:] == GUARD).all()
 
 
-@pytest.mark.parametrize("waves,occ,pf", [(1, -1, 128), (2, -1, 128), (4, -1, 128), (1, 0, 0),
-                                           (1, 20, 1), (2, 12, 3), (1, -1, 100000)])
-def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, pf):
+@pytest.mark.parametrize("waves,occ,pf,sp", [(1, -1, 128, -1), (2, -1, 128, 0), (4, -1, 128, 1), (1, 0, 0, 0),
+                                              (1, 20, 1, 1), (2, 12, 3, 2), (1, -1, 100000, -1)])
+def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, pf, sp):
     gpu_ctx.set_waves_per_block(waves)
     gpu_ctx.set_occupancy(occ, occ)
     gpu_ctx.set_batch_prefetch(pf)
+    gpu_ctx.set_store_policy(sp, sp)
     rnd = random.Random(7)
     sizes = [0, 1, 5, 31, 32, 33, 4095, 4096, 4097, 2**20 + 3, 3 * 2**20, 65536 * 64 + 11]
     sizes += [int(np.exp(rnd.uniform(np.log(4096), np.log(4 * 2**20)))) for _ in range(40)]
@@ -131,6 +132,7 @@ def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, p
     gpu_ctx.set_waves_per_block(0)
     gpu_ctx.set_occupancy(-1, -1)
     gpu_ctx.set_batch_prefetch(128)
+    gpu_ctx.set_store_policy(-1, -1)
 
 
 def test_range_pieces_compose(gpu_ctx, torch, oracle, base):
@@ -150,30 +152,34 @@ def test_store_modes_and_occupancy_agree(gpu_ctx, torch):
     n, size = 40, 2**20 + 4096 * 3
     ref = torch.empty(n * size, dtype=torch.uint8, device="cuda")
     gpu_ctx.fill_stream(ref, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
-    for nt in (False, True):
+    for sp in (-1, 0, 1, 2):
         for waves in (1, 2, 4):
             for cap in (-1, 0, 3, 12, 40):
-                gpu_ctx.set_nontemporal(nt)
+                gpu_ctx.set_store_policy(sp, sp)
                 gpu_ctx.set_waves_per_block(waves)
                 gpu_ctx.set_occupancy(cap, cap)
                 t = torch.zeros_like(ref)
                 gpu_ctx.fill_stream(t, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
-                assert torch.equal(t, ref), (nt, waves, cap)
+                assert torch.equal(t, ref), (sp, waves, cap)
+    gpu_ctx.set_nontemporal(True)
+    t = torch.zeros_like(ref)
+    gpu_ctx.fill_stream(t, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
+    assert torch.equal(t, ref)
     gpu_ctx.set_nontemporal(False)
     gpu_ctx.set_waves_per_block(0)
     gpu_ctx.set_occupancy(-1, -1)
 
 
 def test_occupancy_cap_is_applied(gpu_ctx):
-    # stream default 12 resident 2-wave workgroups per CU, uncapped batch (1 wave)
-    assert gpu_ctx.query_occupancy(batch=False) == 12
+    # stream default 14 resident 2-wave workgroups per CU, uncapped batch (1 wave)
+    assert gpu_ctx.query_occupancy(batch=False) == 14
     assert gpu_ctx.query_occupancy(batch=True) >= 16
     for cap in (8, 10, 16):
         gpu_ctx.set_occupancy(cap, cap)
         assert gpu_ctx.query_occupancy(batch=False) == cap
         assert gpu_ctx.query_occupancy(batch=True) == cap
     gpu_ctx.set_occupancy(-1, -1)
-    assert gpu_ctx.query_occupancy(batch=False) == 12
+    assert gpu_ctx.query_occupancy(batch=False) == 14
 
 
 def test_host_dropin_seeded_multi_chunk(oracle, base):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: fill-kernel launch-shape study on the product library.
 Sweeps the runtime knobs (waves per block, resident-workgroup cap per CU,
-batch tile-record prefetch distance) over cfg4 (log-uniform sizes, batch),
+batch tile-record prefetch distance, store cache policy) over cfg4 (log-uniform sizes, batch),
 cfg7 (uniform 8 MiB, batch) and cfg2 (uniform 8 MiB, stream), interleaved in
 one process, and prints GB/s per point.
 
@@ -14,19 +14,19 @@ sys.path.insert(0, ROOT)
 
 def points():
     spec = os.environ.get("LAB_POINTS")
-    if spec:     # "kind:waves:occ:pf;..."
+    if spec:     # "kind:waves:occ:pf[:store];..."  store: -1 default, 0 plain, 1 nt, 2 sc1
         for p in spec.split(";"):
-            k, w, o, f = p.split(":")
-            yield k, int(w), int(o), int(f)
+            k, w, o, f, *sp = p.split(":")
+            yield k, int(w), int(o), int(f), int(sp[0]) if sp else -1
         return
     for w, o, f in itertools.product([1], [0, 28, 24, 20, 16], [0, 128]):
         for k in ("cfg4", "cfg7"):
-            yield k, w, o, f
+            yield k, w, o, f, -1
     for w, o in [(2, 0), (2, 14), (2, 12)]:
         for k in ("cfg4", "cfg7"):
-            yield k, w, o, 0
+            yield k, w, o, 0, -1
     for w, o in [(2, 0), (2, 14), (2, 12), (1, 0), (1, 24), (1, 20), (1, 16)]:
-        yield "stream2", w, o, 0
+        yield "stream2", w, o, 0, -1
 
 
 def main():
@@ -69,7 +69,8 @@ def main():
     res, occ = {}, {}
     for rep in range(int(os.environ.get("LAB_REPS", "3"))):
         for p in pts:
-            k, w, o, f = p
+            k, w, o, f, sp = p
+            ctx.set_store_policy(sp, sp)
             ctx.set_waves_per_block(w)
             ctx.set_occupancy(o, o)
             ctx.set_batch_prefetch(f)
@@ -80,8 +81,8 @@ def main():
             res.setdefault(p, []).append(descs[k][2] / (e0.elapsed_time(e1) * 1e-3) / 1e9)
         print(f"rep {rep} done", flush=True)
     for p, v in res.items():
-        k, w, o, f = p
-        print(json.dumps({"cfg": k, "waves": w, "occ_cap": o, "wgs_per_cu": occ[p], "pf": f,
+        k, w, o, f, sp = p
+        print(json.dumps({"cfg": k, "waves": w, "occ_cap": o, "wgs_per_cu": occ[p], "pf": f, "store": sp,
                           "GBps_median": round(statistics.median(v), 1), "max": round(max(v), 1)}), flush=True)
 
 
