@@ -84,10 +84,11 @@ int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
  * or mode 1 (DG1, s3dg_dgen_fill and the generators): draws staged per lane
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident
  * workgroups per CU cap (0 = none), minimum draws per lane (>= 64; sets lanes
- * per chunk).  0 = default for each (mode 0: 64, 4; mode 1: 16, 4; 2048).
+ * per chunk), store cache policy (as s3dg_set_store_policy, negative =
+ * default).  0 = default for each (mode 0: 64, 4; mode 1: 16, 4; 2048).
  * A tuning knob; results are identical. */
 int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int wgs_per_cu,
-                             uint64_t min_lane_draws);
+                             uint64_t min_lane_draws, int store_policy);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
 /* Resident workgroups per CU the current settings give (HIP occupancy API). */
 int s3dg_query_occupancy(s3dg_ctx *ctx, int batch, int *wgs_per_cu);

@@ -32,9 +32,10 @@ using namespace s3dg;
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
 constexpr int kDefaultStoreStream = kStoreSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr uint64_t kDefaultKsMinDraws = 2048;
-// measured on MI355X (tools/k2_lab.py): 512-B row pieces for the plain
-// keystream, 128-B pieces for DG1 (zero-prefixed 1 MiB blocks)
-constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0}, {16, 4, 0}};
+// measured on MI355X (tools/k2_lab.py): 512-B row pieces and sc1 stores for
+// the plain keystream, 128-B pieces and plain stores for DG1 (zero-prefixed
+// 1 MiB blocks)
+constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 4, 0, kStorePlain}};
 
 struct s3dg_ctx {
     int device = 0;
@@ -268,7 +269,7 @@ int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
 }
 
 int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wgs_per_cu,
-                             uint64_t min_lane_draws) {
+                             uint64_t min_lane_draws, int store_policy) {
     if (!c) return fail(S3DG_EINVAL, "null context");
     if (mode != 0 && mode != 1) return fail(S3DG_EINVAL, "mode must be 0 (keystream) or 1 (dgen)");
     if (draws != 0 && draws != 16 && draws != 32 && draws != 64)
@@ -276,11 +277,13 @@ int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wg
     if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(S3DG_EINVAL, "waves must be 1, 2 or 4");
     if (wgs_per_cu < 0 || wgs_per_cu > 40) return fail(S3DG_EINVAL, "workgroups per CU must be 0..40");
     if (min_lane_draws != 0 && min_lane_draws < 64) return fail(S3DG_EINVAL, "min_lane_draws must be >= 64");
+    if (store_policy > kStoreSC1) return fail(S3DG_EINVAL, "store policy must be 0, 1, 2 or negative");
     std::lock_guard<std::mutex> g(c->mu);
     const KsShape &def = kDefaultKsShape[mode];
     c->ks[mode].draws = draws ? draws : def.draws;
     c->ks[mode].waves = waves ? waves : def.waves;
     c->ks[mode].wgs_per_cu = wgs_per_cu;
+    c->ks[mode].store = store_policy < 0 ? def.store : store_policy;
     c->ks_min_draws[mode] = min_lane_draws ? min_lane_draws : kDefaultKsMinDraws;
     return S3DG_OK;
 }

@@ -97,9 +97,11 @@ struct KeystreamArgs {
 };
 
 // k_keystream launch shape: draws staged per lane per iteration (16, 32, 64),
-// waves per workgroup (1, 2, 4), resident workgroups per CU cap (0 = none).
+// waves per workgroup (1, 2, 4), resident workgroups per CU cap (0 = none),
+// store cache policy.
 struct KsShape {
     int draws, waves, wgs_per_cu;
+    int store;             // kStorePlain / kStoreNT / kStoreSC1
 };
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
                            const KsShape &sh, hipStream_t s);

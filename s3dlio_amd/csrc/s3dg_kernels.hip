@@ -376,7 +376,7 @@ __device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2
     s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotlk<45>(s3);
 }
 
-template <int D, int W>
+template <int D, int W, int SP>
 __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
     static_assert(D == 16 || D == 32 || D == 64, "draws per stage");
     constexpr int RS = D * 8 + 16;     // row stride: + 16 B pad, conflict-light ds_write_b128 rows
@@ -489,8 +489,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
 #pragma unroll
             for (int i = 0; i < P; ++i) {
                 const uint32_t r = R * i + l / P;
-                *reinterpret_cast<u32x4 *>(dst + raddr[i] + o) =
-                    *reinterpret_cast<const u32x4 *>(myrows + r * RS + piece * 16);
+                store16<SP>(dst + raddr[i] + o, *reinterpret_cast<const u32x4 *>(myrows + r * RS + piece * 16));
             }
         } else {
 #pragma unroll
@@ -500,7 +499,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
                 const u32x4 v = *reinterpret_cast<const u32x4 *>(myrows + r * RS + piece * 16);
                 uint8_t *p = dst + raddr[i] + o;
                 if (o + 16 <= rrem[i]) {
-                    *reinterpret_cast<u32x4 *>(p) = v;
+                    store16<SP>(p, v);
                 } else {
                     const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
                     for (uint32_t b = 0; b < 16 && o + b < rrem[i]; ++b) p[b] = (uint8_t)(dw[b >> 2] >> (8 * (b & 3)));
@@ -515,18 +514,23 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
 
 template <int D, int W>
 hipError_t launch_ks_one(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab, uint32_t lds,
-                         hipStream_t s) {
+                         int store, hipStream_t s) {
     const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
     const uint64_t wgs = (waves + W - 1) / W;
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_keystream<D, W>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+    if (store == kStoreSC1)
+        hipLaunchKernelGGL((k_keystream<D, W, kStoreSC1>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+    else if (store == kStoreNT)
+        hipLaunchKernelGGL((k_keystream<D, W, kStoreNT>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+    else
+        hipLaunchKernelGGL((k_keystream<D, W, kStorePlain>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
     return hipGetLastError();
 }
 
 template <int D, int W>
 hipError_t occ_ks_one(uint32_t lds, int *out) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        out, reinterpret_cast<const void *>(&k_keystream<D, W>), 64 * W, lds);
+        out, reinterpret_cast<const void *>(&k_keystream<D, W, kStorePlain>), 64 * W, lds);
 }
 
 // static LDS of k_keystream<D, W>
@@ -660,7 +664,7 @@ hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t
     (void)hipGetLastError();
     const uint32_t lds = occupancy_lds(sh.wgs_per_cu, ks_static_lds(sh.draws, sh.waves));
     hipError_t e;
-    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, s);
+    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s);
     return e;
 }
 

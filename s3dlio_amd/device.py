@@ -155,11 +155,11 @@ class Context:
         call("s3dg_set_batch_prefetch", self._h, int(tiles))
 
     def set_keystream_shape(self, mode: int, draws: int = 0, waves: int = 0, wgs_per_cu: int = 0,
-                            min_lane_draws: int = 0) -> None:
+                            min_lane_draws: int = 0, store_policy: int = -1) -> None:
         """k_keystream launch shape for mode 0 (npz keystream) or 1 (DG1);
-        0 = default for each; results are identical."""
+        0 (store: -1) = default for each; results are identical."""
         call("s3dg_set_keystream_shape", self._h, int(mode), int(draws), int(waves), int(wgs_per_cu),
-             int(min_lane_draws))
+             int(min_lane_draws), int(store_policy))
 
     def query_keystream_occupancy(self, mode: int = 0) -> int:
         out = ctypes.c_int()

@@ -287,8 +287,8 @@ def test_keystream_vs_oracle(gpu_ctx, torch, oracle, length, chunk, sb):
     assert (h[length:] == GUARD).all()
 
 
-KS_SHAPES = [(16, 4, 0, 0), (16, 1, 0, 0), (32, 2, 0, 0), (64, 4, 0, 0), (64, 1, 3, 0),
-             (64, 2, 0, 4096), (32, 4, 1, 64), (16, 2, 0, 128)]
+KS_SHAPES = [(16, 4, 0, 0, -1), (16, 1, 0, 0, 2), (32, 2, 0, 0, 1), (64, 4, 0, 0, 2), (64, 1, 3, 0, 0),
+             (64, 2, 0, 4096, -1), (32, 4, 1, 64, 2), (16, 2, 0, 128, 1)]
 
 
 @pytest.mark.parametrize("shape", KS_SHAPES)

@@ -3,7 +3,8 @@
 keystream and DG1 dgen mode), interleaved in one process.
 
     LAB_POINTS="16:4:0:2048;64:1:0:2048" python tools/k2_lab.py     # GPU box
-Point = draws-per-stage : waves-per-workgroup : workgroups-per-CU cap : min draws per lane.
+Point = draws-per-stage : waves-per-workgroup : workgroups-per-CU cap : min draws per lane
+        [: store policy (-1 default, 0 plain, 1 nt, 2 sc1)].
 Tooling only: nothing in the product imports this."""
 import json, os, statistics, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,6 +26,7 @@ def main():
     st = torch.cuda.current_stream()
     sh = int(st.cuda_stream)
     pts = [tuple(int(x) for x in p.split(":")) for p in os.environ.get("LAB_POINTS", DEFAULT).split(";")]
+    pts = [p if len(p) == 5 else p + (-1,) for p in pts]
 
     def run(kind):
         if kind == "k2":
@@ -44,7 +46,7 @@ def main():
                 res.setdefault((p, kind), []).append(n / (e0.elapsed_time(e1) * 1e-3) / 1e9)
         print(f"rep {rep} done", flush=True)
     for (p, kind), v in res.items():
-        print(json.dumps({"kind": kind, "draws": p[0], "waves": p[1], "cap": p[2], "min_draws": p[3],
+        print(json.dumps({"kind": kind, "draws": p[0], "waves": p[1], "cap": p[2], "min_draws": p[3], "store": p[4],
                           "wgs_per_cu": occ[p], "GBps_median": round(statistics.median(v), 1),
                           "max": round(max(v), 1)}), flush=True)
 
