@@ -226,8 +226,18 @@ class DataGenerator:
         self.instance_entropy = int(seed)
 
     @classmethod
+    def new(cls, seed: int | None = None) -> "DataGenerator":
+        """DataGenerator::new(Option<u64>) (src/data_gen.rs:262-264)."""
+        return cls(seed)
+
+    @classmethod
     def new_with_seed(cls, seed: int) -> "DataGenerator":
         return cls(seed)
+
+    @classmethod
+    def default(cls) -> "DataGenerator":
+        """impl Default for DataGenerator: new(None) (src/data_gen.rs:301-305)."""
+        return cls(None)
 
     def begin_object(self, size: int, dedup: int, compress: int) -> ObjectGen:
         return ObjectGen(size, dedup, compress, self.instance_entropy)

@@ -115,6 +115,11 @@ def test_datagenerator_instances(S):
     b = g.begin_object(2 * MiB, 1, 1).fill_remaining()
     c = S.DataGenerator().begin_object(2 * MiB, 1, 1).fill_remaining()
     assert a == b and a != c
+    # new(Some(s)) == new_with_seed(s); default() == new(None)
+    s1 = S.DataGenerator.new(7).begin_object(MiB, 2, 2).fill_remaining()
+    s2 = S.DataGenerator.new_with_seed(7).begin_object(MiB, 2, 2).fill_remaining()
+    assert s1 == s2
+    assert S.DataGenerator.default().begin_object(MiB, 1, 1).fill_remaining() != s1
 
 
 @pytest.mark.parametrize("size", [100, 64 * 1024, 3 * MiB + 17])
