@@ -6,17 +6,18 @@ import ctypes, json, os, statistics, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
-VARIANTS = ["0", "2", "0 -DS3DG_NW=2", "2 -DS3DG_NW=2", "0 -DS3DG_NW=1", "2 -DS3DG_NW=1"]
+VARIANTS = ["0", "1", "2", "3"]     # S3DG_ABLATE bits: 1 = no window patch, 2 = no PRNG chain
 
 
 def build():
     os.makedirs(OUT, exist_ok=True)
-    srcs = [os.path.join(ROOT, "s3dlio_amd", "csrc", f) for f in ("s3dg_kernels.hip", "s3dg_capi.cpp")]
+    from s3dlio_amd.build import SOURCES
     for k in VARIANTS:
-        so = os.path.join(OUT, f"libablate{k.replace(' ', '_').replace('=', '')}.so")
+        so = os.path.join(OUT, f"libablate{k}.so")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                               "-shared", *f"-DS3DG_ABLATE={k}".split(), "-I", os.path.join(ROOT, "include"),
-                               "-I", os.path.join(ROOT, "s3dlio_amd", "csrc"), "-o", so] + srcs)
+                               "-shared", f"-DS3DG_ABLATE={k}", "-mllvm", "-amdgpu-kernarg-preload-count=16",
+                               "-I", os.path.join(ROOT, "include"),
+                               "-I", os.path.join(ROOT, "s3dlio_amd", "csrc"), "-o", so] + SOURCES)
 
 
 def main():
@@ -25,7 +26,7 @@ def main():
     import torch
     libs = {}
     for k in VARIANTS:
-        L = ctypes.CDLL(os.path.join(OUT, f"libablate{k.replace(' ', '_').replace('=', '')}.so"), mode=os.RTLD_LOCAL)
+        L = ctypes.CDLL(os.path.join(OUT, f"libablate{k}.so"), mode=os.RTLD_LOCAL)
         h = ctypes.c_void_p()
         assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
         libs[k] = (L, h)
