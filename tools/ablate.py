@@ -30,7 +30,7 @@ def main():
         h = ctypes.c_void_p()
         assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
         libs[k] = (L, h)
-    size, n = 8 << 20, 2048
+    size, n = 8 << 20, 8192
     buf = torch.empty(n * size, dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream(); sh = ctypes.c_void_p(st.cuda_stream)
     u64 = ctypes.c_uint64
@@ -39,16 +39,22 @@ def main():
         r = L.s3dg_fill_controlled_stream(h, ctypes.c_void_p(buf.data_ptr()), u64(size), u64(size), u64(n),
                                           u64(d), ctypes.c_uint32(fn), ctypes.c_uint32(fd), u64(1), u64(0), sh)
         assert r == 0
+    shapes = [(2, 14), (2, 12), (2, 10), (2, 8), (1, 16), (1, 12), (1, 8), (4, 4), (4, 6)]
     res = {}
-    for _ in range(5):
+    for _ in range(3):
         for k in VARIANTS:
-            for (d, fn, fd) in [(1, 0, 1), (4, 1, 2), (2, 2, 3)]:
-                run(k, d, fn, fd)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st); run(k, d, fn, fd); e1.record(st); torch.cuda.synchronize()
-                res.setdefault((k, d, fd), []).append(buf.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9)
-    for (k, d, fd), v in res.items():
-        print(json.dumps({"ablate": k, "dedup": d, "f_den": fd, "GBps": round(statistics.median(v), 1)}))
+            for w, cap in shapes:
+                L, h = libs[k]
+                assert L.s3dg_set_waves_per_block(h, w) == 0
+                assert L.s3dg_set_occupancy(h, cap, cap) == 0
+                for (d, fn, fd) in [(1, 0, 1)]:
+                    run(k, d, fn, fd)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st); run(k, d, fn, fd); e1.record(st); torch.cuda.synchronize()
+                    res.setdefault((k, w, cap, d, fd), []).append(buf.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    for (k, w, cap, d, fd), v in res.items():
+        print(json.dumps({"ablate": k, "waves": w, "cap": cap, "dedup": d, "f_den": fd,
+                          "GBps": round(statistics.median(v), 1)}))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Diagnostic: A/B of compile-time kernel variants on the same workloads,
+interleaved in one process.  Each variant is the product library built with
+extra -D flags (LAB_VARIANTS="name=-DFOO=1 -DBAR=2;name2=").  Points as in
+tools/batch_lab.py: "kind:waves:occ:pf:store;..." with kind in
+stream2 (cfg2 stream), stream3 (cfg3 stream), cfg4 (log-uniform batch),
+cfg7 (uniform 8 MiB batch), ceiling (store-only kernel).
+
+    LAB_VARIANTS=... python tools/variant_lab.py --build-only   # here
+    LAB_VARIANTS=... LAB_POINTS=... python tools/variant_lab.py # GPU box
+Tooling only: nothing in the product imports this."""
+import ctypes, json, os, statistics, subprocess, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tools", "_build")
+
+
+def variants():
+    spec = os.environ.get("LAB_VARIANTS", "base=")
+    out = {}
+    for item in spec.split(";"):
+        name, _, flags = item.partition("=")
+        out[name.strip()] = flags.split()
+    return out
+
+
+def so(name):
+    return os.path.join(OUT, f"libvariant_{name}.so")
+
+
+def build():
+    from s3dlio_amd.build import SOURCES, CSRC
+    os.makedirs(OUT, exist_ok=True)
+    procs = []
+    for name, flags in variants().items():
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-mllvm", "-amdgpu-kernarg-preload-count=16", "-I", os.path.join(ROOT, "include"),
+               "-I", CSRC, "-DS3DG_BUILD", *flags, "-o", so(name)] + SOURCES
+        procs.append(subprocess.Popen(cmd))
+        if len(procs) >= 4:
+            assert procs.pop(0).wait() == 0
+    for p in procs:
+        assert p.wait() == 0
+
+
+def main():
+    if "--build-only" in sys.argv:
+        build()
+        return
+    import torch
+    from bench import log_uniform_sizes, SEED_BASE
+    from s3dlio_amd._lib import ObjDesc
+    MiB = 1 << 20
+    n = int(os.environ.get("LAB_N", "10000"))
+    u64, u32 = ctypes.c_uint64, ctypes.c_uint32
+    libs = {}
+    for name in variants():
+        L = ctypes.CDLL(so(name), mode=os.RTLD_LOCAL)
+        h = ctypes.c_void_p()
+        assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
+        libs[name] = (L, h)
+    descs = {}
+    for kind, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3), ("cfg7", [8 * MiB] * n, 1, 0, 1)]:
+        arr = (ObjDesc * n)()
+        off = 0
+        for j, sz in enumerate(sizes):
+            arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), d, fn, fd)
+            off += (sz + 4095) // 4096 * 4096
+        descs[kind] = (arr, sum(sizes))
+    work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "ceiling": 8 * MiB * n,
+            "cfg4": descs["cfg4"][1], "cfg7": descs["cfg7"][1]}
+    buf = torch.empty(8 * MiB * n, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    sh = ctypes.c_void_p(st.cuda_stream)
+    p = ctypes.c_void_p(buf.data_ptr())
+
+    def run(L, h, kind):
+        if kind in ("stream2", "stream3"):
+            d, fn, fd = (1, 0, 1) if kind == "stream2" else (4, 1, 2)
+            r = L.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(d), u32(fn), u32(fd),
+                                              u64(SEED_BASE), u64(0), sh)
+        elif kind == "ceiling":
+            r = L.s3dg_write_ceiling(h, p, u64(8 * MiB * n), u32(0xA5A5A5A5), sh)
+        else:
+            r = L.s3dg_fill_controlled_batch(h, p, descs[kind][0], u64(n), sh)
+        assert r == 0
+    pts = []
+    for item in os.environ.get("LAB_POINTS", "stream2:2:-1:128:-1;cfg4:1:-1:128:-1").split(";"):
+        k, w, o, f, sp = item.split(":")
+        pts.append((k, int(w), int(o), int(f), int(sp)))
+    res = {}
+    for rep in range(int(os.environ.get("LAB_REPS", "4"))):
+        for pt in pts:
+            for name, (L, h) in libs.items():
+                k, w, o, f, sp = pt
+                assert L.s3dg_set_waves_per_block(h, w) == 0
+                assert L.s3dg_set_occupancy(h, o, o) == 0
+                assert L.s3dg_set_batch_prefetch(h, u32(f)) == 0
+                assert L.s3dg_set_store_policy(h, sp, sp) == 0
+                run(L, h, k)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st); run(L, h, k); e1.record(st); torch.cuda.synchronize()
+                res.setdefault((name, pt), []).append(work[k] / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+        print(f"rep {rep} done", flush=True)
+    for (name, pt), v in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+        print(json.dumps({"variant": name, "point": ":".join(map(str, pt)),
+                          "GBps_median": round(statistics.median(v), 1), "max": round(max(v), 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
