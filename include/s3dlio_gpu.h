@@ -255,6 +255,15 @@ int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_t n, uint64
                      int object_type, int payload, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                      uint64_t seed_base, uint32_t max_in_flight, uint32_t *crc_out,
                      s3dg_put_stats *stats);
+/* Same over several contexts (GPUs): object j is generated by context
+ * j * nctx / n's lane (contiguous ranges), each lane with its own device
+ * chunks, streams and pinned ring on its GPU's NUMA node, one shared writer
+ * pool.  Files and checksums are identical for any nctx; two contexts on one
+ * device run two lanes on it. */
+int s3dg_put_objects_multi(s3dg_ctx *const *ctxs, uint32_t nctx, const char *const *paths,
+                           uint64_t n, uint64_t size, int object_type, int payload, uint64_t dedup,
+                           uint32_t f_num, uint32_t f_den, uint64_t seed_base, uint32_t max_in_flight,
+                           uint32_t *crc_out, s3dg_put_stats *stats);
 
 /* ---- host-buffer drop-ins (src/data_gen.rs:151 signature) ---------------- */
 /* generate_random_data(size) (src/data_gen.rs:102): seeded analogue layout

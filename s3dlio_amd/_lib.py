@@ -118,6 +118,9 @@ SIGNATURES = {
     "s3dlio_generate_random_data": (c_int, [c_vp, ctypes.c_size_t]),
     "s3dg_put_objects": (c_int, [c_vp, ctypes.POINTER(ctypes.c_char_p), c_u64, c_u64, c_int, c_int,
                                  c_u64, c_u32, c_u32, c_u64, c_u32, c_vp, ctypes.POINTER(PutStats)]),
+    "s3dg_put_objects_multi": (c_int, [ctypes.POINTER(c_vp), c_u32, ctypes.POINTER(ctypes.c_char_p), c_u64,
+                                       c_u64, c_int, c_int, c_u64, c_u32, c_u32, c_u64, c_u32, c_vp,
+                                       ctypes.POINTER(PutStats)]),
     "s3dg_last_error": (ctypes.c_char_p, []),
     "s3dg_version": (ctypes.c_char_p, []),
 }

@@ -37,7 +37,9 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <array>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -68,7 +70,8 @@ constexpr uint64_t kSlotBytes = 256ull << 20;   // device chunk / host slot (mul
 constexpr int kHostSlots = 4;
 constexpr uint64_t kMaxRegions = kSlotBytes / kBlk + kSlotBytes / (256 * 1024) + 16;
 
-// Process-wide buffers, created on first use; one put runs at a time.
+// Process-wide buffers per (device, lane), created on first use and reused;
+// a lane's pool is held (mutex) for the duration of a call.
 struct PutPool {
     std::mutex mu;
     bool ready = false;
@@ -82,8 +85,13 @@ struct PutPool {
     void *crc_tab = nullptr;
 };
 
-PutPool &pool() {
-    static PutPool *p = new PutPool();   // never destroyed: HIP may be torn down first at exit
+PutPool &pool(int device, int lane) {
+    // never destroyed: HIP may be torn down first at exit
+    static std::mutex *mu = new std::mutex();
+    static std::map<std::pair<int, int>, PutPool *> *pools = new std::map<std::pair<int, int>, PutPool *>();
+    std::lock_guard<std::mutex> g(*mu);
+    PutPool *&p = (*pools)[{device, lane}];
+    if (!p) p = new PutPool();
     return *p;
 }
 
@@ -168,14 +176,14 @@ struct Job {
     std::vector<uint8_t> pre, suf;   // framing: pre at file offset 0, suf right after the data
     const uint8_t *data = nullptr;
     uint64_t len = 0, data_off = 0;  // payload bytes at file offset data_off
-    int slot = -1;
+    int lane = 0, slot = -1;         // pinned ring slot of the payload (-1: none)
 };
 
 struct Writers {
     std::mutex mu;
     std::condition_variable cv_job, cv_slot;
     std::deque<Job> q;
-    int outstanding[kHostSlots] = {};
+    std::vector<std::array<int, kHostSlots>> outstanding;   // per lane, per ring slot
     bool closing = false;
     std::atomic<bool> failed{false};
     std::string err;
@@ -200,7 +208,7 @@ struct Writers {
             if (!failed.load()) do_write(j);
             if (j.slot >= 0) {
                 std::lock_guard<std::mutex> g(mu);
-                if (--outstanding[j.slot] == 0) cv_slot.notify_all();
+                if (--outstanding[j.lane][j.slot] == 0) cv_slot.notify_all();
             }
         }
     }
@@ -240,15 +248,15 @@ struct Writers {
     void push(Job &&j) {
         {
             std::lock_guard<std::mutex> g(mu);
-            if (j.slot >= 0) ++outstanding[j.slot];
+            if (j.slot >= 0) ++outstanding[j.lane][j.slot];
             q.push_back(std::move(j));
         }
         cv_job.notify_one();
     }
 
-    void wait_slot(int s) {
+    void wait_slot(int lane, int s) {
         std::unique_lock<std::mutex> lk(mu);
-        cv_slot.wait(lk, [&] { return outstanding[s] == 0; });
+        cv_slot.wait(lk, [&] { return outstanding[lane][s] == 0; });
     }
 
     void finish() {
@@ -295,14 +303,169 @@ double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+struct PutArgs {
+    const char *const *paths;
+    uint64_t n, size;
+    int object_type, payload;
+    uint64_t dedup;
+    uint32_t f_num, f_den;
+    uint64_t seed_base;
+    uint32_t *crc_out;
+    uint64_t pre_len;
+};
+
+void frame_job(const PutArgs &A, uint64_t j, uint32_t pcrc, Job &job) {
+    object_frame(A.object_type, 1, A.size, pcrc, job.pre, job.suf);
+    if (A.crc_out) {
+        uint32_t c = crc32_host_update(0, job.pre.data(), job.pre.size());
+        c = job.pre.empty() ? pcrc : crc32_combine(c, pcrc, A.size);
+        if (!job.suf.empty()) c = crc32_combine(c, crc32_host_update(0, job.suf.data(), job.suf.size()), job.suf.size());
+        A.crc_out[j] = c;
+    }
+}
+
+// One lane: objects [j0, j1) on one device through its own pool: chunk c ->
+// device slot c&1 / stream c&1 -> pinned host slot c % kHostSlots -> writers.
+int run_lane(const PutArgs &A, s3dg_ctx *ctx, PutPool &P, int lane, uint64_t j0, uint64_t j1, Writers &W,
+             double &gpu_wait) {
+    const uint64_t size = A.size;
+    const uint64_t stride = (size + kBlk - 1) / kBlk * kBlk;
+    std::vector<ChunkDesc> chunks;
+    if (stride <= kSlotBytes) {
+        const uint64_t K = kSlotBytes / stride;
+        for (uint64_t j = j0; j < j1; j += K) {
+            ChunkDesc c;
+            c.first_obj = j;
+            c.n_objs = j1 - j < K ? j1 - j : K;
+            c.len = size;
+            chunks.push_back(c);
+        }
+    } else {
+        for (uint64_t j = j0; j < j1; ++j)
+            for (uint64_t off = 0; off < size; off += kSlotBytes) {
+                ChunkDesc c;
+                c.first_obj = j;
+                c.n_objs = 1;
+                c.off = off;
+                c.len = size - off < kSlotBytes ? size - off : kSlotBytes;
+                c.piece = true;
+                chunks.push_back(c);
+            }
+    }
+    const uint64_t nbD = (size + kDgenBlock - 1) / kDgenBlock;
+    std::shared_ptr<OpenFile> cur_file;   // split object being written
+    uint32_t cur_crc = 0;
+
+    auto enqueue = [&](uint64_t ci) -> int {
+        const ChunkDesc &c = chunks[ci];
+        const int ds = (int)(ci & 1), hs = (int)(ci % kHostSlots);
+        hipStream_t s = P.st[ds];
+        uint8_t *d = (uint8_t *)P.dev[ds];
+        if (A.payload == S3DG_PAYLOAD_DGEN) {        // one launch for the whole chunk
+            const uint64_t b0 = c.off / kDgenBlock, b1 = (c.off + c.len + kDgenBlock - 1) / kDgenBlock;
+            if (int r = s3dg_internal_dgen_chunk(ctx, d, size, stride, c.n_objs, c.piece ? b0 : 0,
+                                                 c.piece ? b1 : nbD, A.dedup, A.f_num, A.f_den, A.seed_base,
+                                                 c.first_obj, s))
+                return r;
+        } else {
+            const uint64_t b0 = c.off / kBlk, b1 = (c.off + c.len + kBlk - 1) / kBlk;
+            if (int r = s3dg_internal_fill_chunk(ctx, d, size, stride, c.n_objs, b0, b1,
+                                                 A.payload == S3DG_PAYLOAD_RANDOM, A.dedup, A.f_num, A.f_den,
+                                                 A.seed_base, c.first_obj, s))
+                return r;
+        }
+        const CrcSegPlan cp = crc_seg_plan(c.n_objs, c.len, stride);
+        if (cp.nreg > kMaxRegions) return s3dg_internal_fail(S3DG_EINVAL, "crc region table overflow");
+        PUT_HIP(crc_seg_launch(cp, d, P.crc_tab, P.dev_reg[ds], s), "launch k_crc32_regions");
+        W.wait_slot(lane, hs);                             // writers done with chunk ci - kHostSlots
+        if (cp.nreg)
+            PUT_HIP(hipMemcpyAsync(P.host_reg[hs], P.dev_reg[ds], cp.nreg * 4, hipMemcpyDeviceToHost, s),
+                    "hipMemcpyAsync(crc regions)");
+        const uint64_t bytes = (c.n_objs - 1) * stride + c.len;
+        PUT_HIP(hipMemcpyAsync(P.host[hs], d, bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync(D2H payload)");
+        PUT_HIP(hipEventRecord(P.ev[hs], s), "hipEventRecord");
+        return S3DG_OK;
+    };
+
+    auto complete = [&](uint64_t ci) -> int {
+        const ChunkDesc &c = chunks[ci];
+        const int hs = (int)(ci % kHostSlots);
+        const double tw = now_s();
+        PUT_HIP(hipEventSynchronize(P.ev[hs]), "hipEventSynchronize(put chunk)");
+        gpu_wait += now_s() - tw;
+        const CrcSegPlan cp = crc_seg_plan(c.n_objs, c.len, stride);
+        std::vector<const uint8_t *> tails(c.n_objs);
+        for (uint64_t k = 0; k < c.n_objs; ++k) tails[k] = P.host[hs] + k * stride + cp.seg_rows * 1024;
+        std::vector<uint32_t> crcs(c.n_objs);
+        crc_seg_fold(cp, P.host_reg[hs], tails.data(), crcs.data());
+        if (!c.piece) {
+            for (uint64_t k = 0; k < c.n_objs; ++k) {
+                const uint64_t j = c.first_obj + k;
+                Job job;
+                job.path = A.paths[j];
+                frame_job(A, j, crcs[k], job);
+                job.data = P.host[hs] + k * stride;
+                job.len = size;
+                job.data_off = A.pre_len;
+                job.lane = lane;
+                job.slot = hs;
+                W.push(std::move(job));
+            }
+            return S3DG_OK;
+        }
+        const uint64_t j = c.first_obj;
+        if (c.off == 0) {
+            cur_file = std::make_shared<OpenFile>();
+            cur_file->fd = open_create(A.paths[j]);
+            if (cur_file->fd < 0) {
+                W.fail(std::string("open ") + A.paths[j] + ": " + strerror(errno));
+                return S3DG_OK;
+            }
+            cur_crc = crcs[0];
+        } else {
+            cur_crc = crc32_combine(cur_crc, crcs[0], c.len);
+        }
+        Job job;
+        job.path = A.paths[j];
+        job.of = cur_file;
+        job.data = P.host[hs];
+        job.len = c.len;
+        job.data_off = A.pre_len + c.off;
+        job.lane = lane;
+        job.slot = hs;
+        if (c.off + c.len == size) {                       // last piece: framing with the full CRC
+            frame_job(A, j, cur_crc, job);
+            W.files += 1;                                  // closed when the last piece job drops it
+            cur_file.reset();
+        }
+        W.push(std::move(job));
+        return S3DG_OK;
+    };
+
+    int rc = S3DG_OK;
+    for (uint64_t ci = 0; ci < chunks.size() && rc == S3DG_OK && !W.failed.load(); ++ci) {
+        if ((rc = enqueue(ci)) != S3DG_OK) break;
+        if (ci > 0) rc = complete(ci - 1);
+    }
+    if (rc == S3DG_OK && !W.failed.load() && !chunks.empty()) rc = complete(chunks.size() - 1);
+    cur_file.reset();
+    // drain the GPU before the pinned ring can be reused by the next call
+    (void)hipStreamSynchronize(P.st[0]);
+    (void)hipStreamSynchronize(P.st[1]);
+    return rc;
+}
+
 }  // namespace
 
-extern "C" int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_t n, uint64_t size,
-                                int object_type, int payload, uint64_t dedup, uint32_t f_num,
-                                uint32_t f_den, uint64_t seed_base, uint32_t max_in_flight,
-                                uint32_t *crc_out, s3dg_put_stats *stats) {
+extern "C" int s3dg_put_objects_multi(s3dg_ctx *const *ctxs, uint32_t nctx, const char *const *paths,
+                                      uint64_t n, uint64_t size, int object_type, int payload, uint64_t dedup,
+                                      uint32_t f_num, uint32_t f_den, uint64_t seed_base,
+                                      uint32_t max_in_flight, uint32_t *crc_out, s3dg_put_stats *stats) {
     const double t0 = now_s();
-    if (!ctx) return s3dg_internal_fail(S3DG_EINVAL, "null context");
+    if (!ctxs || nctx == 0) return s3dg_internal_fail(S3DG_EINVAL, "no context");
+    if (nctx > 64) return s3dg_internal_fail(S3DG_EINVAL, "at most 64 contexts");
+    for (uint32_t k = 0; k < nctx; ++k)
+        if (!ctxs[k]) return s3dg_internal_fail(S3DG_EINVAL, "null context");
     if (n && !paths) return s3dg_internal_fail(S3DG_EINVAL, "null path list");
     for (uint64_t j = 0; j < n; ++j)
         if (!paths[j] || !paths[j][0]) return s3dg_internal_fail(S3DG_EINVAL, "empty path");
@@ -318,14 +481,23 @@ extern "C" int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_
     if (stats) *stats = s3dg_put_stats{0, 0, 0.0, 0.0};
     if (n == 0) return S3DG_OK;
 
-    int dev = 0;
-    if (int r = s3dg_internal_ctx_device(ctx, &dev)) return r;
-    PutPool &P = pool();
-    std::lock_guard<std::mutex> plk(P.mu);
-    if (int r = pool_init(P, dev)) return r;
-    PUT_HIP(hipSetDevice(dev), "hipSetDevice");
+    // lanes: one per context, each on its own (device, lane) pool
+    const uint32_t L = (uint64_t)nctx < n ? nctx : (uint32_t)n;
+    std::vector<int> devs(L);
+    std::vector<PutPool *> pools(L);
+    std::vector<std::unique_lock<std::mutex>> locks;
+    std::map<int, int> lane_of_dev;
+    for (uint32_t k = 0; k < L; ++k) {
+        if (int r = s3dg_internal_ctx_device(ctxs[k], &devs[k])) return r;
+        pools[k] = &pool(devs[k], lane_of_dev[devs[k]]++);
+    }
+    for (uint32_t k = 0; k < L; ++k) {
+        locks.emplace_back(pools[k]->mu);
+        if (int r = pool_init(*pools[k], devs[k])) return r;
+    }
 
     Writers W;
+    W.outstanding.assign(L, std::array<int, kHostSlots>{});
     uint32_t nthreads = max_in_flight == 0 ? 64 : (max_in_flight > 512 ? 512 : max_in_flight);
     // file writes are memcpy into the page cache: more writers than CPUs only
     // contend (measured: 64 writers on a 16-CPU share run at half the rate of 16)
@@ -334,152 +506,56 @@ extern "C" int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_
     const uint32_t nw = (uint64_t)nthreads < n ? nthreads : (uint32_t)n;
     for (uint32_t k = 0; k < nw; ++k) W.th.emplace_back([&W] { W.run(); });
 
-    std::vector<uint8_t> pre0, suf0;
-    object_frame(object_type, 1, size, 0, pre0, suf0);       // sizes of the framing
-    const uint64_t pre_len = pre0.size();
-    double gpu_wait = 0.0;
-
-    auto frame_job = [&](uint64_t j, uint32_t pcrc, Job &job) {
-        object_frame(object_type, 1, size, pcrc, job.pre, job.suf);
-        if (crc_out) {
-            uint32_t c = crc32_host_update(0, job.pre.data(), job.pre.size());
-            c = job.pre.empty() ? pcrc : crc32_combine(c, pcrc, size);
-            if (!job.suf.empty()) c = crc32_combine(c, crc32_host_update(0, job.suf.data(), job.suf.size()), job.suf.size());
-            crc_out[j] = c;
-        }
-    };
+    PutArgs A{paths, n, size, object_type, payload, dedup, f_num, f_den, seed_base, crc_out, 0};
+    {
+        std::vector<uint8_t> pre0, suf0;
+        object_frame(object_type, 1, size, 0, pre0, suf0);       // sizes of the framing
+        A.pre_len = pre0.size();
+    }
 
     int rc = S3DG_OK;
+    double gpu_wait = 0.0;
     if (size == 0) {                       // framing only: no GPU work
         for (uint64_t j = 0; j < n; ++j) {
             Job job;
             job.path = paths[j];
-            frame_job(j, 0, job);
+            frame_job(A, j, 0, job);
             job.data_off = job.pre.size();
             W.push(std::move(job));
         }
     } else {
-        // ---- chunk plan
-        const uint64_t stride = (size + kBlk - 1) / kBlk * kBlk;
-        std::vector<ChunkDesc> chunks;
-        if (stride <= kSlotBytes) {
-            const uint64_t K = kSlotBytes / stride;
-            for (uint64_t j = 0; j < n; j += K) {
-                ChunkDesc c;
-                c.first_obj = j;
-                c.n_objs = n - j < K ? n - j : K;
-                c.len = size;
-                chunks.push_back(c);
+        // contiguous object ranges per lane; each lane's thread runs near its GPU
+        std::vector<int> lrc(L, S3DG_OK);
+        std::vector<double> lwait(L, 0.0);
+        std::vector<std::string> lerr(L);
+        auto lane_main = [&](uint32_t k) {
+            NumaScope numa(devs[k]);
+            if (hipSetDevice(devs[k]) != hipSuccess) {
+                lrc[k] = s3dg_internal_fail(S3DG_EHIP, "hipSetDevice");
+            } else {
+                const uint64_t q = n / L, r = n % L;
+                const uint64_t j0 = k * q + (k < r ? k : r), j1 = j0 + q + (k < r ? 1 : 0);
+                lrc[k] = run_lane(A, ctxs[k], *pools[k], (int)k, j0, j1, W, lwait[k]);
             }
+            if (lrc[k] != S3DG_OK) {
+                lerr[k] = s3dg_last_error();   // thread-local: carry it to the caller's thread
+                W.fail(lerr[k]);
+            }
+        };
+        if (L == 1) {
+            lane_main(0);
         } else {
-            for (uint64_t j = 0; j < n; ++j)
-                for (uint64_t off = 0; off < size; off += kSlotBytes) {
-                    ChunkDesc c;
-                    c.first_obj = j;
-                    c.n_objs = 1;
-                    c.off = off;
-                    c.len = size - off < kSlotBytes ? size - off : kSlotBytes;
-                    c.piece = true;
-                    chunks.push_back(c);
-                }
+            std::vector<std::thread> lt;
+            for (uint32_t k = 0; k < L; ++k) lt.emplace_back(lane_main, k);
+            for (auto &t : lt) t.join();
         }
-        const uint64_t nbD = (size + kDgenBlock - 1) / kDgenBlock;
-        std::shared_ptr<OpenFile> cur_file;   // split object being written
-        uint32_t cur_crc = 0;
-
-        auto enqueue = [&](uint64_t ci) -> int {
-            const ChunkDesc &c = chunks[ci];
-            const int ds = (int)(ci & 1), hs = (int)(ci % kHostSlots);
-            hipStream_t s = P.st[ds];
-            uint8_t *d = (uint8_t *)P.dev[ds];
-            if (payload == S3DG_PAYLOAD_DGEN) {        // one launch for the whole chunk
-                const uint64_t b0 = c.off / kDgenBlock, b1 = (c.off + c.len + kDgenBlock - 1) / kDgenBlock;
-                if (int r = s3dg_internal_dgen_chunk(ctx, d, size, stride, c.n_objs, c.piece ? b0 : 0,
-                                                     c.piece ? b1 : nbD, dedup, f_num, f_den, seed_base,
-                                                     c.first_obj, s))
-                    return r;
-            } else {
-                const uint64_t b0 = c.off / kBlk, b1 = (c.off + c.len + kBlk - 1) / kBlk;
-                if (int r = s3dg_internal_fill_chunk(ctx, d, size, stride, c.n_objs, b0, b1,
-                                                     payload == S3DG_PAYLOAD_RANDOM, dedup, f_num, f_den,
-                                                     seed_base, c.first_obj, s))
-                    return r;
+        for (uint32_t k = 0; k < L; ++k) {
+            if (lwait[k] > gpu_wait) gpu_wait = lwait[k];
+            if (rc == S3DG_OK && lrc[k] != S3DG_OK) {
+                rc = lrc[k];
+                s3dg_internal_fail(rc, lerr[k].c_str());
             }
-            const CrcSegPlan cp = crc_seg_plan(c.n_objs, c.len, stride);
-            if (cp.nreg > kMaxRegions) return s3dg_internal_fail(S3DG_EINVAL, "crc region table overflow");
-            PUT_HIP(crc_seg_launch(cp, d, P.crc_tab, P.dev_reg[ds], s), "launch k_crc32_regions");
-            W.wait_slot(hs);                                   // writers done with chunk ci - kHostSlots
-            if (cp.nreg)
-                PUT_HIP(hipMemcpyAsync(P.host_reg[hs], P.dev_reg[ds], cp.nreg * 4, hipMemcpyDeviceToHost, s),
-                        "hipMemcpyAsync(crc regions)");
-            const uint64_t bytes = (c.n_objs - 1) * stride + c.len;
-            PUT_HIP(hipMemcpyAsync(P.host[hs], d, bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync(D2H payload)");
-            PUT_HIP(hipEventRecord(P.ev[hs], s), "hipEventRecord");
-            return S3DG_OK;
-        };
-
-        auto complete = [&](uint64_t ci) -> int {
-            const ChunkDesc &c = chunks[ci];
-            const int hs = (int)(ci % kHostSlots);
-            const double tw = now_s();
-            PUT_HIP(hipEventSynchronize(P.ev[hs]), "hipEventSynchronize(put chunk)");
-            gpu_wait += now_s() - tw;
-            const CrcSegPlan cp = crc_seg_plan(c.n_objs, c.len, stride);
-            std::vector<const uint8_t *> tails(c.n_objs);
-            for (uint64_t k = 0; k < c.n_objs; ++k) tails[k] = P.host[hs] + k * stride + cp.seg_rows * 1024;
-            std::vector<uint32_t> crcs(c.n_objs);
-            crc_seg_fold(cp, P.host_reg[hs], tails.data(), crcs.data());
-            if (!c.piece) {
-                for (uint64_t k = 0; k < c.n_objs; ++k) {
-                    const uint64_t j = c.first_obj + k;
-                    Job job;
-                    job.path = paths[j];
-                    frame_job(j, crcs[k], job);
-                    job.data = P.host[hs] + k * stride;
-                    job.len = size;
-                    job.data_off = pre_len;
-                    job.slot = hs;
-                    W.push(std::move(job));
-                }
-                return S3DG_OK;
-            }
-            const uint64_t j = c.first_obj;
-            if (c.off == 0) {
-                cur_file = std::make_shared<OpenFile>();
-                cur_file->fd = open_create(paths[j]);
-                if (cur_file->fd < 0) {
-                    W.fail(std::string("open ") + paths[j] + ": " + strerror(errno));
-                    return S3DG_OK;
-                }
-                cur_crc = crcs[0];
-            } else {
-                cur_crc = crc32_combine(cur_crc, crcs[0], c.len);
-            }
-            Job job;
-            job.path = paths[j];
-            job.of = cur_file;
-            job.data = P.host[hs];
-            job.len = c.len;
-            job.data_off = pre_len + c.off;
-            job.slot = hs;
-            if (c.off + c.len == size) {                       // last piece: framing with the full CRC
-                frame_job(j, cur_crc, job);
-                W.files += 1;                                  // closed when the last piece job drops it
-                cur_file.reset();
-            }
-            W.push(std::move(job));
-            return S3DG_OK;
-        };
-
-        for (uint64_t ci = 0; ci < chunks.size() && rc == S3DG_OK && !W.failed.load(); ++ci) {
-            if ((rc = enqueue(ci)) != S3DG_OK) break;
-            if (ci > 0) rc = complete(ci - 1);
         }
-        if (rc == S3DG_OK && !W.failed.load() && !chunks.empty()) rc = complete(chunks.size() - 1);
-        cur_file.reset();
-        // drain the GPU before the pinned ring can be reused by the next call
-        (void)hipStreamSynchronize(P.st[0]);
-        (void)hipStreamSynchronize(P.st[1]);
     }
     W.finish();
     if (rc == S3DG_OK && W.failed.load()) rc = s3dg_internal_fail(S3DG_EIO, W.err.c_str());
@@ -490,4 +566,12 @@ extern "C" int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_
         stats->gpu_seconds = gpu_wait;
     }
     return rc;
+}
+
+extern "C" int s3dg_put_objects(s3dg_ctx *ctx, const char *const *paths, uint64_t n, uint64_t size,
+                                int object_type, int payload, uint64_t dedup, uint32_t f_num,
+                                uint32_t f_den, uint64_t seed_base, uint32_t max_in_flight,
+                                uint32_t *crc_out, s3dg_put_stats *stats) {
+    return s3dg_put_objects_multi(&ctx, 1, paths, n, size, object_type, payload, dedup, f_num, f_den,
+                                  seed_base, max_in_flight, crc_out, stats);
 }

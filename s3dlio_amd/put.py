@@ -74,11 +74,38 @@ class PutResult:
         return f"crc32c:{self.checksums[j]:08x}"
 
 
-def put_objects(uris, size: int, max_in_flight: int = 64, config: Config | None = None,
-                seed: int | None = None, payload: str | None = None, context=None) -> PutResult:
-    """Generate one payload per URI on the GPU and write the files."""
-    import numpy as np
+def _contexts(devices):
+    """Contexts for `devices`: None / "all" = every visible GPU, else a list of
+    device indices (repeats give several lanes on one GPU)."""
+    from .device import Context
     from .npz import default_context
+    if devices is None or devices == "all":
+        n = ctypes.c_int()
+        call("s3dg_device_count", ctypes.byref(n))
+        devices = list(range(max(1, n.value)))
+    ctxs = []
+    for d in devices:
+        if d == 0 and not any(c.device == 0 for c in ctxs):
+            ctxs.append(default_context())
+        else:
+            key = (int(d), sum(1 for c in ctxs if c.device == int(d)))
+            if key not in _LANE_CTX:
+                _LANE_CTX[key] = Context(int(d))
+            ctxs.append(_LANE_CTX[key])
+    return ctxs
+
+
+_LANE_CTX: dict = {}
+
+
+def put_objects(uris, size: int, max_in_flight: int = 64, config: Config | None = None,
+                seed: int | None = None, payload: str | None = None, context=None,
+                devices=None) -> PutResult:
+    """Generate one payload per URI on the GPU(s) and write the files.
+    `context` pins the call to one GPU; otherwise `devices` (default: every
+    visible GPU) each take a contiguous range of the objects.  Output files
+    and checksums do not depend on the GPU count."""
+    import numpy as np
     cfg = config or Config.new_with_defaults(ObjectType.RAW, 1, size, 1, 1)
     if cfg.object_type == ObjectType.HDF5:
         raise ValueError("HDF5 format is not available in this build")
@@ -94,9 +121,10 @@ def put_objects(uris, size: int, max_in_flight: int = 64, config: Config | None 
     arr = (ctypes.c_char_p * max(1, n))(*[p.encode() for p in paths])
     crcs = np.zeros(max(1, n), np.uint32)
     st = PutStats()
-    ctx = context or default_context()
-    call("s3dg_put_objects", ctx._h, arr, n, int(size), int(cfg.object_type), kind, dedup, fn, fd,
-         int(seed) & (2**64 - 1), int(max_in_flight), int(crcs.ctypes.data), ctypes.byref(st))
+    ctxs = [context] if context is not None else _contexts(devices)
+    harr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    call("s3dg_put_objects_multi", harr, len(ctxs), arr, n, int(size), int(cfg.object_type), kind, dedup,
+         fn, fd, int(seed) & (2**64 - 1), int(max_in_flight), int(crcs.ctypes.data), ctypes.byref(st))
     return PutResult([int(c) for c in crcs[:n]], st.objects, st.bytes, st.seconds, st.gpu_seconds,
                      int(seed) & (2**64 - 1))
 
@@ -110,7 +138,8 @@ def put_objects_with_random_data_and_type(uris, size: int, max_in_flight: int, c
 def put(prefix: str, num: int, template: str | None = None, max_in_flight: int = 64,
         size: int | None = None, should_create_bucket: bool = False, object_type: str = "zeros",
         dedup_factor: int = 1, compress_factor: int = 1, data_gen_algorithm: str = "random",
-        data_gen_mode: str = "streaming", chunk_size: int = 262144, seed: int | None = None) -> None:
+        data_gen_mode: str = "streaming", chunk_size: int = 262144, seed: int | None = None,
+        devices=None) -> None:
     """python_core_api.rs:777-818.  should_create_bucket: parents are always
     created for file:// (file_store.rs:562-564); data_gen_algorithm: only
     "random" exists (prand deprecated, :696-701)."""
@@ -122,4 +151,4 @@ def put(prefix: str, num: int, template: str | None = None, max_in_flight: int =
     cfg = (Config.new_with_defaults(ObjectType.from_str(object_type), 1, sz, dedup_factor,
                                     compress_factor)
            .with_data_gen_mode(mode).with_chunk_size(chunk_size))
-    put_objects(uris, sz, jobs, cfg, seed)
+    put_objects(uris, sz, jobs, cfg, seed, devices=devices)

@@ -176,6 +176,40 @@ def test_gpu_put_io_error_is_loud(S, gpu_ctx, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,t,n,size,d,c", [
+    ("controlled", "RAW", 70, 3 * MiB + 5, 2, 3),
+    ("dgen", "TFRECORD", 9, 2 * MiB + 17, 2, 2),
+    ("controlled", "NPZ", 3, 300 * MiB + 9, 1, 3),        # split objects on every lane
+])
+def test_gpu_put_lanes_give_identical_files(S, oracle, golden_base, gpu_ctx, tmp_path, kind, t, n, size, d, c):
+    """s3dg_put_objects_multi: 1, 2 and 3 lanes (contexts) on this GPU write
+    the same files and return the same checksums (object j's bytes depend
+    only on (seed, j)); spot-check against the oracle."""
+    cfg = S.Config.new_with_defaults(t, 1, size, d, c)
+    res = {}
+    for lanes in (1, 2, 3):
+        out = tmp_path / f"l{lanes}"
+        uris = [f"file://{out}/o-{j}" for j in range(n)]
+        r = S.put_objects(uris, size, 16, cfg, seed=77, payload=kind, devices=[0] * lanes)
+        assert r.objects == n
+        res[lanes] = (r.checksums, [zlib.crc32(open(f"{out}/o-{j}", "rb").read()) for j in range(n)])
+        assert res[lanes][0] == res[lanes][1]
+    assert res[1] == res[2] == res[3]
+    j = n - 1
+    got = open(f"{tmp_path}/l3/o-{j}", "rb").read()
+    assert got == _frame(t, size, _expect(oracle, golden_base, kind, size, d, c, 77, j))
+
+
+@pytest.mark.gpu
+def test_gpu_put_lane_error_is_loud(S, gpu_ctx, tmp_path):
+    blocker = tmp_path / "file"
+    blocker.write_bytes(b"x")
+    uris = [f"file://{tmp_path}/ok-{j}" for j in range(5)] + [f"file://{blocker}/bad"]
+    with pytest.raises(OSError):
+        S.put_objects(uris, 8192, seed=1, devices=[0, 0])
+
+
+@pytest.mark.gpu
 def test_numa_local_pinned_alloc_roundtrip():
     """s3dg_host_alloc_pinned_local: pinned memory on the GPU's NUMA node,
     usable as a D2H target."""

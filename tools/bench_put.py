@@ -56,15 +56,18 @@ def main():
         shutil.rmtree(f"{root}/warm")
         out = [{"what": f"fs write ceiling: {n} x 8 MiB from one host buffer, 16 threads",
                 "GiBps": fs_ceiling(root, n, size)}]
+        lanes = [int(x) for x in os.environ.get("PUT_LANES", "1").split(",")]
         for kind, d, c in [("controlled", 1, 1), ("random", 1, 1), ("dgen", 2, 3)]:
             for mif in (16, 64):
-                uris = [f"file://{root}/p/o{j}" for j in range(n)]
-                cfg = S.Config.new_with_defaults("RAW", 1, size, d, c)
-                r = S.put_objects(uris, size, mif, cfg, seed=3, payload=kind)
-                out.append({"what": f"put_objects {n} x 8 MiB {kind} d{d} c{c}, max_in_flight={mif}",
-                            "GiBps": r.bytes / r.seconds / GiB, "seconds": r.seconds,
-                            "gpu_wait_seconds": r.gpu_seconds})
-                shutil.rmtree(f"{root}/p")
+                for nl in lanes:
+                    uris = [f"file://{root}/p/o{j}" for j in range(n)]
+                    cfg = S.Config.new_with_defaults("RAW", 1, size, d, c)
+                    r = S.put_objects(uris, size, mif, cfg, seed=3, payload=kind, devices=[0] * nl)
+                    out.append({"what": f"put_objects {n} x 8 MiB {kind} d{d} c{c}, max_in_flight={mif}, "
+                                        f"{nl} lane(s) on GPU 0",
+                                "GiBps": r.bytes / r.seconds / GiB, "seconds": r.seconds,
+                                "gpu_wait_seconds": r.gpu_seconds})
+                    shutil.rmtree(f"{root}/p")
         for o in out:
             print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in o.items()}))
     finally:
