@@ -287,8 +287,11 @@ def main() -> int:
 
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["size"] is not None:
-        cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("keystream"):
+        if cfg["size"] is not None:
+            cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds)
+        else:
+            cpu = cpu_baseline_batch(cfg, fn, fd, args.cpu_seconds, sizes)
 
     if rank == 0:
         out = {
@@ -389,6 +392,63 @@ def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=1024, per_
     return {"value": round(n_objs * size / dt / GiB, 2), "unit": "GiB/s",
             "sample": f"{n_objs} x {size // MiB} MiB objects, 2 x {per_chunk}-object device chunks, "
                       f"pinned host ring on NUMA node {node.value}, generate || D2H on two streams"}
+
+
+def cpu_baseline_batch(cfg, fn, fd, seconds, sizes):
+    """Mixed-size configs: the C restatement per object (s3dgo_fill_controlled),
+    objects spread over a pool of host threads, each writing into its own reused
+    buffer; the same object sizes and parameters as the GPU run."""
+    import ctypes
+    import threading
+    import numpy as np
+    from oracle import oracle_c as OC
+    threads = max(1, min(16, os.cpu_count() or 1))
+    base = OC.base_block(BASE_SEED)
+    L = OC.lib()
+    cap = max(sizes)
+    lock = threading.Lock()
+    state = {"next": 0, "bytes": 0, "objs": 0, "stop": False}
+
+    def worker():
+        buf = np.ones(cap, np.uint8)                     # faulted in before timing starts
+        bp = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        pp = base.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        done = nobj = 0
+        start.wait()
+        while not state["stop"]:
+            with lock:
+                j = state["next"]
+                state["next"] += 1
+            sz = sizes[j % len(sizes)]
+            L.s3dgo_fill_controlled(bp, sz, cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, j), pp)
+            done += sz
+            nobj += 1
+        with lock:
+            state["bytes"] += done
+            state["objs"] += nobj
+    start = threading.Event()
+    ts = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in ts:
+        t.start()
+    time.sleep(0.5)                                       # buffers allocated and touched
+    t0 = time.perf_counter()
+    start.set()
+    time.sleep(seconds)
+    state["stop"] = True
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    return {"value": round(state["bytes"] / dt / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{state['objs']} objects of the config's sizes ({state['bytes'] / GiB:.0f} GiB) over "
+                      f"{dt:.1f} s, one object per task on {threads} threads, reused host buffers; {model}"}
+
+
+def object_entropy_py(seed_base: int, j: int) -> int:
+    return (seed_base + (j << 32)) & (2**64 - 1)
 
 
 def cpu_baseline(cfg, fn, fd, seconds):
