@@ -83,8 +83,8 @@ int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
 /* Keystream kernel launch shape for mode 0 (npz keystream, s3dg_xoshiro_fill)
  * or mode 1 (DG1, s3dg_dgen_fill and the generators): draws staged per lane
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident
- * workgroups per CU cap (0 = none), minimum draws per lane (>= 64; sets lanes
- * per chunk), store cache policy (as s3dg_set_store_policy, negative =
+ * workgroups per CU cap (0 = none), draws per lane (>= 64; sets lanes per
+ * chunk; launches too small to fill the GPU use shorter spans, down to 256), store cache policy (as s3dg_set_store_policy, negative =
  * default).  0 = default for each (mode 0: 64, 4; mode 1: 16, 4; 2048).
  * A tuning knob; results are identical. */
 int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int wgs_per_cu,

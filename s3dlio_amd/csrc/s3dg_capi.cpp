@@ -32,6 +32,7 @@ using namespace s3dg;
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
 constexpr int kDefaultStoreStream = kStoreSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr uint64_t kDefaultKsMinDraws = 2048;
+constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
 // measured on MI355X (tools/k2_lab.py): 512-B row pieces and sc1 stores for
 // the plain keystream, 128-B pieces and plain stores for DG1 (zero-prefixed
 // 1 MiB blocks)
@@ -39,6 +40,7 @@ constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 4, 0, kStore
 
 struct s3dg_ctx {
     int device = 0;
+    int cus = 256;                     // compute units (sizes small keystream launches)
     // store cache policy: sc1 (write, then drop the line from L2) measured best
     int store_stream = kDefaultStoreStream, store_batch = kDefaultStoreBatch;
     int waves_per_block = 0;           // 0 = auto: 2 for streams, 1 for batches (measured)
@@ -181,6 +183,9 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
     HIP_TRY(hipSetDevice(device), "hipSetDevice");
     s3dg_ctx *c = new s3dg_ctx();
     c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->cus = cus;
     hipError_t e = hipMalloc(&c->base_dev, kBlk);
     if (e != hipSuccess) { delete c; return hipfail(e, "hipMalloc(base block)"); }
     e = hipEventCreateWithFlags(&c->tab_free, hipEventDisableTiming);
@@ -459,7 +464,7 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
 }
 
 // lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
-static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, KeystreamArgs &A,
+static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t nchunks, KeystreamArgs &A,
                           const uint64_t **jtab) {
     const uint64_t nd = chunk_bytes / 8;
     // as many lanes per chunk as keep >= ks_min_draws draws per lane (the
@@ -467,6 +472,11 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, Keystream
     const uint64_t min_draws = c->ks_min_draws[mode];
     uint32_t lpc = 1;
     while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
+    // small launches (a few chunks): spread each chunk over more lanes, down
+    // to 256 draws per lane, until the grid has ~4 waves per CU; otherwise a
+    // 8 MiB request runs as 16 long waves and is latency-bound
+    const uint64_t target_lanes = (uint64_t)c->cus * 4 * 64;
+    while (lpc < 1024 && nchunks * lpc < target_lanes && nd / (2 * lpc) >= kKsMinSpan) lpc *= 2;
     uint64_t span = (nd + lpc - 1) / lpc;
     const uint64_t D = (uint64_t)c->ks[mode].draws;    // a lane stages D draws per iteration
     span = (span + D - 1) / D * D;
@@ -499,7 +509,7 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, 0, chunk_bytes, A, &jt)) return r;
+    if (int r = keystream_plan(c, 0, chunk_bytes, (len + chunk_bytes - 1) / chunk_bytes, A, &jt)) return r;
     A.nchunks = (len + chunk_bytes - 1) / chunk_bytes;
     A.chunk_bytes = chunk_bytes;
     A.obj_len = len;
@@ -541,7 +551,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, 1, kDgenBlock, A, &jt)) return r;
+    if (int r = keystream_plan(c, 1, kDgenBlock, (blk_hi - blk_lo) * n_objs, A, &jt)) return r;
     const uint64_t U = s3dg_unique_blocks(nb, dedup);
     A.cpo = blk_hi - blk_lo;
     A.nchunks = A.cpo * n_objs;
@@ -661,10 +671,11 @@ namespace {
 struct DefaultCtx {
     std::mutex mu;
     s3dg_ctx *ctx = nullptr;
-    uint8_t proc_base[kBlk];           // A_BASE_BLOCK equivalent (random, once per process)
-    bool have_proc_base = false;
-    uint8_t proc_base2[kBlk];          // BASE_BLOCK equivalent (src/constants.rs:725-729)
-    bool have_proc_base2 = false;
+    // base blocks in HBM, each uploaded once: A_BASE_BLOCK (random, once per
+    // process, src/constants.rs:715-720), BASE_BLOCK (:725-729), and the
+    // caller's block of a seeded call (re-uploaded per call; calls are
+    // serialised by `mu` and each drains its streams before returning)
+    void *base_proc = nullptr, *base_proc2 = nullptr, *base_user = nullptr;
     void *scratch[2] = {nullptr, nullptr};
     hipStream_t st[2] = {nullptr, nullptr};
     static constexpr uint64_t kChunk = 64ull << 20;   // 64 MiB per device chunk
@@ -675,32 +686,44 @@ DefaultCtx &dflt() {
     return *d;
 }
 
+int random_bytes(uint8_t *dst, size_t n);
+
 int dflt_init(DefaultCtx &D) {
     if (D.ctx) return S3DG_OK;
     int dev = 0;
     if (const char *e = getenv("S3DLIO_GPU_DEVICE")) dev = atoi(e);
-    if (int r = s3dg_ctx_create(dev, &D.ctx)) return r;
+    s3dg_ctx *c = nullptr;
+    if (int r = s3dg_ctx_create(dev, &c)) return r;
     for (int k = 0; k < 2; ++k) {
         HIP_TRY(hipMalloc(&D.scratch[k], DefaultCtx::kChunk), "hipMalloc(scratch)");
         HIP_TRY(hipStreamCreateWithFlags(&D.st[k], hipStreamNonBlocking), "hipStreamCreate");
     }
+    uint8_t b[kBlk];
+    HIP_TRY(hipMalloc(&D.base_user, kBlk), "hipMalloc(base block)");
+    HIP_TRY(hipMalloc(&D.base_proc, kBlk), "hipMalloc(base block)");
+    if (int r = random_bytes(b, kBlk)) return r;
+    HIP_TRY(hipMemcpy(D.base_proc, b, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
+    HIP_TRY(hipMalloc(&D.base_proc2, kBlk), "hipMalloc(base block)");
+    if (int r = random_bytes(b, kBlk)) return r;
+    HIP_TRY(hipMemcpy(D.base_proc2, b, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
+    D.ctx = c;
     return S3DG_OK;
 }
 
 // Generate into a host buffer through two 64 MiB device chunks on two
-// streams, so chunk k+1's kernel overlaps chunk k's D2H copy.
-int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t dedup, uint64_t compress,
-              uint64_t entropy) {
-    uint32_t fn, fd;
-    if (int r = s3dg_compress_ratio(compress, &fn, &fd)) return r;
+// streams, so chunk k+1's kernel overlaps chunk k's D2H copy.  `pp` selects
+// the layout (controlled, or f_den = 0: generate_random_data's); `base` is
+// the device base block.
+int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, const PrefixParams &pp, uint64_t entropy,
+              const void *base) {
     const uint64_t nb = (len + kBlk - 1) / kBlk;
     const uint64_t cb = DefaultCtx::kChunk / kBlk;
     for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
         const uint64_t b1 = b0 + cb < nb ? b0 + cb : nb;
         const int sl = (int)(k & 1);
-        if (int r = s3dg_fill_controlled_range(D.ctx, D.scratch[sl], len, b0, b1, dedup, fn, fd,
-                                               entropy, D.st[sl]))
-            return r;
+        HIP_TRY(launch_fill_stream(cfg_for(D.ctx), (uint8_t *)D.scratch[sl], len, 0, 1, (uint32_t)b0,
+                                   (uint32_t)b1, entropy, 0, pp, base, D.st[sl]),
+                "launch k_fill_stream(host chunk)");
         const uint64_t off = b0 * kBlk;
         const uint64_t n = (b1 * kBlk < len ? b1 * kBlk : len) - off;
         HIP_TRY(hipMemcpyAsync(buf + off, D.scratch[sl], n, hipMemcpyDeviceToHost, D.st[sl]),
@@ -711,9 +734,19 @@ int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t dedup, uint64_
     return S3DG_OK;
 }
 
-// generate_random_data layout (seeded analogue) into a host buffer, chunked
-// like fill_host; block i seeded entropy + i.
-int fill_host_random(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t entropy) {
+int fill_host_controlled(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t dedup, uint64_t compress,
+                         uint64_t entropy, const void *base) {
+    uint32_t fn, fd;
+    if (int r = s3dg_compress_ratio(compress, &fn, &fd)) return r;
+    const uint64_t nb = (len + kBlk - 1) / kBlk;
+    PrefixParams pp;
+    if (int r = make_prefix(nb, dedup, fn, fd, &pp)) return r;
+    return fill_host(D, buf, len, pp, entropy, base);
+}
+
+// generate_random_data layout (seeded analogue) into a host buffer; block i
+// seeded entropy + i.
+int fill_host_random(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t entropy, const void *base) {
     const uint64_t nb = (len + kBlk - 1) / kBlk;
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
     PrefixParams pp{};
@@ -721,21 +754,7 @@ int fill_host_random(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t entropy
     pp.f_den = 0;
     pp.m_unique = fastmod_magic(1);
     pp.m_fden = fastmod_magic(1);
-    const uint64_t cb = DefaultCtx::kChunk / kBlk;
-    for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
-        const uint64_t b1 = b0 + cb < nb ? b0 + cb : nb;
-        const int sl = (int)(k & 1);
-        HIP_TRY(launch_fill_stream(cfg_for(D.ctx), (uint8_t *)D.scratch[sl], len, 0, 1, (uint32_t)b0,
-                                   (uint32_t)b1, entropy, 0, pp, D.ctx->base_dev, D.st[sl]),
-                "launch k_fill_stream(random data)");
-        const uint64_t off = b0 * kBlk;
-        const uint64_t n = (b1 * kBlk < len ? b1 * kBlk : len) - off;
-        HIP_TRY(hipMemcpyAsync(buf + off, D.scratch[sl], n, hipMemcpyDeviceToHost, D.st[sl]),
-                "hipMemcpyAsync(D2H)");
-    }
-    HIP_TRY(hipStreamSynchronize(D.st[0]), "hipStreamSynchronize");
-    HIP_TRY(hipStreamSynchronize(D.st[1]), "hipStreamSynchronize");
-    return S3DG_OK;
+    return fill_host(D, buf, len, pp, entropy, base);
 }
 
 int random_bytes(uint8_t *dst, size_t n) {
@@ -775,17 +794,8 @@ int s3dg_internal_random_host(uint8_t *buf, uint64_t len, uint64_t entropy, int 
     DefaultCtx &D = dflt();
     std::lock_guard<std::mutex> g(D.mu);
     if (int r = dflt_init(D)) return r;
-    if (!use_process_base) return fill_host_random(D, buf, len, entropy);
-    if (!D.have_proc_base2) {
-        if (int r = random_bytes(D.proc_base2, kBlk)) return r;
-        D.have_proc_base2 = true;
-    }
-    uint8_t saved[kBlk];
-    std::memcpy(saved, D.ctx->base_host, kBlk);
-    if (int r = s3dg_set_base_block(D.ctx, D.proc_base2)) return r;
-    int r = fill_host_random(D, buf, len, time_entropy());
-    int r2 = s3dg_set_base_block(D.ctx, saved);
-    return r ? r : r2;
+    if (!use_process_base) return fill_host_random(D, buf, len, entropy, D.ctx->base_dev);
+    return fill_host_random(D, buf, len, time_entropy(), D.base_proc2);
 }
 
 int s3dlio_generate_random_data(uint8_t *buf, size_t size) {
@@ -800,16 +810,7 @@ int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t c
     DefaultCtx &D = dflt();
     std::lock_guard<std::mutex> g(D.mu);
     if (int r = dflt_init(D)) return r;
-    if (!D.have_proc_base) {
-        if (int r = random_bytes(D.proc_base, kBlk)) return r;
-        D.have_proc_base = true;
-    }
-    uint8_t saved[kBlk];
-    std::memcpy(saved, D.ctx->base_host, kBlk);
-    if (int r = s3dg_set_base_block(D.ctx, D.proc_base)) return r;
-    int r = fill_host(D, buf, len, dedup, compress, time_entropy());
-    int r2 = s3dg_set_base_block(D.ctx, saved);
-    return r ? r : r2;
+    return fill_host_controlled(D, buf, len, dedup, compress, time_entropy(), D.base_proc);
 }
 
 int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, size_t compress,
@@ -819,13 +820,12 @@ int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, s
     DefaultCtx &D = dflt();
     std::lock_guard<std::mutex> g(D.mu);
     if (int r = dflt_init(D)) return r;
-    if (!base4096) return fill_host(D, buf, len, dedup, compress, entropy);
-    uint8_t saved[kBlk];
-    std::memcpy(saved, D.ctx->base_host, kBlk);
-    if (int r = s3dg_set_base_block(D.ctx, base4096)) return r;
-    int r = fill_host(D, buf, len, dedup, compress, entropy);
-    int r2 = s3dg_set_base_block(D.ctx, saved);
-    return r ? r : r2;
+    const void *base = D.ctx->base_dev;
+    if (base4096) {
+        HIP_TRY(hipMemcpy(D.base_user, base4096, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
+        base = D.base_user;
+    }
+    return fill_host_controlled(D, buf, len, dedup, compress, entropy, base);
 }
 
 }  // extern "C"
