@@ -31,12 +31,13 @@ using namespace s3dg;
 
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
 constexpr int kDefaultStoreStream = kStoreSC1, kDefaultStoreBatch = kStoreSC1;
-constexpr uint64_t kDefaultKsMinDraws = 2048;
+constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
 // measured on MI355X (tools/k2_lab.py): 512-B row pieces and sc1 stores for
-// the plain keystream, 128-B pieces and plain stores for DG1 (zero-prefixed
-// 1 MiB blocks)
-constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 4, 0, kStorePlain}};
+// the plain keystream; 128-B pieces, 2-wave workgroups, 1024 draws per lane
+// and plain stores for DG1 (zero-prefixed 1 MiB blocks: with 128 lanes per
+// block, whole waves fall inside the prefix and skip the PRNG)
+constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 2, 0, kStorePlain}};
 
 struct s3dg_ctx {
     int device = 0;
@@ -50,7 +51,7 @@ struct s3dg_ctx {
     uint32_t prefetch_tiles = 128;     // batch tile-record prefetch distance
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
-    uint64_t ks_min_draws[2] = {kDefaultKsMinDraws, kDefaultKsMinDraws};   // >= draws per lane
+    uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // batch descriptor table (device) + pinned staging, grown on demand
@@ -289,7 +290,7 @@ int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wg
     c->ks[mode].waves = waves ? waves : def.waves;
     c->ks[mode].wgs_per_cu = wgs_per_cu;
     c->ks[mode].store = store_policy < 0 ? def.store : store_policy;
-    c->ks_min_draws[mode] = min_lane_draws ? min_lane_draws : kDefaultKsMinDraws;
+    c->ks_min_draws[mode] = min_lane_draws ? min_lane_draws : kDefaultKsMinDraws[mode];
     return S3DG_OK;
 }
 

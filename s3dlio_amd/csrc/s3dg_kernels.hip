@@ -421,6 +421,43 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     }
     uint64_t s0 = mix64(x + 0x9E3779B97F4A7C15ull), s1 = mix64(x + 2 * 0x9E3779B97F4A7C15ull);
     uint64_t s2 = mix64(x + 3 * 0x9E3779B97F4A7C15ull), s3 = mix64(x + 4 * 0x9E3779B97F4A7C15ull);
+    const uint64_t d0 = (uint64_t)sub * span;                        // first draw index
+    const uint32_t iters = span / D;
+    const uint32_t piece = l % P;
+    // destination of the P rows this lane helps write: row R*i + l/P, piece l%P
+    uint64_t raddr[P];
+    uint32_t rrem[P];
+    auto row_dest = [&]() {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            const uint32_t r = R * i + l / P;
+            raddr[i] = __shfl(coff + rb, (int)r);
+            rrem[i] = __shfl(rlen, (int)r);
+        }
+    };
+    const bool full_rows = __all(rlen == span * 8u);
+
+    // A wave whose regions all lie inside their chunks' zero prefixes (DG1,
+    // compress > 1) stores zeros: no jump, no PRNG.
+    if (__all(rlen == 0 || rb + rlen <= zlen)) {
+        row_dest();
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        for (uint32_t it = 0; it < iters; ++it) {
+            const uint32_t o = it * (D * 8) + piece * 16;
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                if (full_rows) {
+                    store16<SP>(dst + raddr[i] + o, z);
+                } else if (o < rrem[i]) {
+                    uint8_t *q = dst + raddr[i] + o;
+                    if (o + 16 <= rrem[i]) store16<SP>(q, z);
+                    else for (uint32_t b = 0; o + b < rrem[i]; ++b) q[b] = 0;
+                }
+            }
+        }
+        return;
+    }
+
     if (lpc > 1 && sub > 0) {                    // jump to draw sub*span
         const uint64_t *J = jtab + 4 * sub;
         const uint64_t j0 = J[0], j1 = J[1], j2 = J[2], j3 = J[3];
@@ -433,23 +470,11 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         }
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
+    row_dest();
 
-    // destination of the P rows this lane helps write: row R*i + l/P, piece l%P
-    const uint32_t piece = l % P;
-    uint64_t raddr[P];
-    uint32_t rrem[P];
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        const uint32_t r = R * i + l / P;
-        raddr[i] = __shfl(coff + rb, (int)r);
-        rrem[i] = __shfl(rlen, (int)r);
-    }
-    const uint64_t d0 = (uint64_t)sub * span;                        // first draw index
-    const uint32_t iters = span / D;
     // Wave-uniform fast paths: a D-draw group needs no masking when no lane
     // of the wave is inside a zero prefix or at its chunk's 1-4 byte tail;
     // the stores need no guards when every region of the wave is full length.
-    const bool full_rows = __all(rlen == span * 8u);
     // Per lane: iterations < it_plain may touch the zero prefix (draws below
     // ceil(zlen/8)); iteration it_tail holds the 1-4 byte tail draw.
     const uint64_t zdraws = (zlen + 7) >> 3;
