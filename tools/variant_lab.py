@@ -4,7 +4,7 @@ interleaved in one process.  Each variant is the product library built with
 extra -D flags (LAB_VARIANTS="name=-DFOO=1 -DBAR=2;name2=").  Points as in
 tools/batch_lab.py: "kind:waves:occ:pf:store;..." with kind in
 stream2 (cfg2 stream), stream3 (cfg3 stream), cfg4 (log-uniform batch),
-cfg7 (uniform 8 MiB batch), ceiling (store-only kernel).
+cfg7 (uniform 8 MiB batch), ceiling (store-only kernel), crc (s3dg_crc32).
 
     LAB_VARIANTS=... python tools/variant_lab.py --build-only   # here
     LAB_VARIANTS=... LAB_POINTS=... python tools/variant_lab.py # GPU box
@@ -67,7 +67,8 @@ def main():
             arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), d, fn, fd)
             off += (sz + 4095) // 4096 * 4096
         descs[kind] = (arr, sum(sizes))
-    work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "ceiling": 8 * MiB * n,
+    crcs = {}
+    work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
             "cfg4": descs["cfg4"][1], "cfg7": descs["cfg7"][1]}
     buf = torch.empty(8 * MiB * n, dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
@@ -81,6 +82,10 @@ def main():
                                               u64(SEED_BASE), u64(0), sh)
         elif kind == "ceiling":
             r = L.s3dg_write_ceiling(h, p, u64(8 * MiB * n), u32(0xA5A5A5A5), sh)
+        elif kind == "crc":                  # synchronous: device regions + host fold
+            out = u32()
+            r = L.s3dg_crc32(h, p, u64(8 * MiB * n), sh, ctypes.byref(out))
+            crcs.setdefault(L, set()).add(out.value)
         else:
             r = L.s3dg_fill_controlled_batch(h, p, descs[kind][0], u64(n), sh)
         assert r == 0
@@ -98,10 +103,18 @@ def main():
                 assert L.s3dg_set_batch_prefetch(h, u32(f)) == 0
                 assert L.s3dg_set_store_policy(h, sp, sp) == 0
                 run(L, h, k)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st); run(L, h, k); e1.record(st); torch.cuda.synchronize()
-                res.setdefault((name, pt), []).append(work[k] / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+                torch.cuda.synchronize()
+                if k == "crc":
+                    import time
+                    t0 = time.perf_counter(); run(L, h, k); dt = time.perf_counter() - t0
+                else:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st); run(L, h, k); e1.record(st); torch.cuda.synchronize()
+                    dt = e0.elapsed_time(e1) * 1e-3
+                res.setdefault((name, pt), []).append(work[k] / dt / 1e9)
         print(f"rep {rep} done", flush=True)
+    if crcs:
+        print(json.dumps({"crc_values_per_variant": {n: sorted(crcs.get(libs[n][0], [])) for n in libs}}))
     for (name, pt), v in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
         print(json.dumps({"variant": name, "point": ":".join(map(str, pt)),
                           "GBps_median": round(statistics.median(v), 1), "max": round(max(v), 1)}), flush=True)
