@@ -96,8 +96,24 @@ def sha(b) -> str:
     return hashlib.sha256(bytes(b)).hexdigest()
 
 
+def launch_ranks(n: int) -> int:
+    """`--gpus N` outside torch.distributed.run: start the N ranks as a child
+    torch.distributed.run (one process per GPU) and return its exit code.
+    Nothing here has touched the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main() -> int:
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus)
     import torch
     from s3dlio_amd import Context, compress_ratio, object_entropy
     from s3dlio_amd._lib import ObjDesc, lib, call
