@@ -126,3 +126,43 @@ def test_generator_config_validation_cpu():
     assert (c.dedup_factor, c.compress_factor, c.numa_mode, c.seed) == (1, 1, S.NumaMode.AUTO, None)
     with pytest.raises(ValueError, match="block_size"):
         S.generate_data_from_config(S.GeneratorConfig(10, block_size=4096))
+
+
+def test_header_is_plain_c_and_links(tmp_path):
+    """include/s3dlio_gpu.h is a C header (C99 and C++11 clean), and a C
+    program links against the library: host math answers, and with no GPU
+    creating a context is an error with a message, not a fallback."""
+    import shutil
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("gcc not available")
+    subprocess.check_call([gcc, "-fsyntax-only", "-x", "c", "-std=c99", "-Wall", "-Wextra", "-pedantic",
+                           "-Werror", HEADER])
+    subprocess.check_call(["g++", "-fsyntax-only", "-x", "c++", "-std=c++11", "-Wall", "-Werror", HEADER])
+    from s3dlio_amd._lib import LIB_PATH
+    src = tmp_path / "t.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include "s3dlio_gpu.h"
+int main(void) {
+    uint32_t fn = 0, fd = 0;
+    if (s3dg_unique_blocks(2048, 4) != 512) return 1;
+    if (s3dg_compress_ratio(3, &fn, &fd) != 0 || fn != 2 || fd != 3) return 2;
+    if (s3dg_object_entropy(1, 2) != 1 + (2ull << 32)) return 3;
+    s3dg_ctx *c = 0;
+    int r = s3dg_ctx_create(0, &c);
+    printf("%d|%s\n", r, r ? s3dg_last_error() : "ok");
+    if (r == 0) s3dg_ctx_destroy(c);
+    return 0;
+}
+''')
+    exe = tmp_path / "t"
+    libdir = os.path.dirname(LIB_PATH)
+    subprocess.check_call([gcc, "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HEADER), str(src),
+                           "-L", libdir, "-ls3dlio_amd", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out
+    code, msg = out.stdout.strip().split("|", 1)
+    import torch
+    if not torch.cuda.is_available():
+        assert int(code) < 0 and msg
