@@ -77,8 +77,8 @@ def parse():
     p.add_argument("--ring-gib", type=float, default=80.0,
                    help="device output ring per GPU (objects wrap when the step exceeds it)")
     p.add_argument("--waves-per-block", type=int, default=None, help="1, 2 or 4 (default 2)")
-    p.add_argument("--store", choices=["default", "plain", "nt", "sc1"], default="default",
-                   help="fill-kernel store cache policy (default: library's, sc1)")
+    p.add_argument("--store", choices=["default", "plain", "nt", "sc1", "ntsc1"], default="default",
+                   help="fill-kernel store cache policy (default: library's, nt sc1 stream / sc1 batch)")
     p.add_argument("--occupancy", type=int, default=None,
                    help="resident fill workgroups per CU cap (default: library's, 14 stream / none batch)")
     p.add_argument("--prefetch", type=int, default=None,
@@ -125,7 +125,7 @@ def main() -> int:
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
     ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block)
-    store = {"default": -1, "plain": 0, "nt": 1, "sc1": 2}[args.store]
+    store = {"default": -1, "plain": 0, "nt": 1, "sc1": 2, "ntsc1": 3}[args.store]
     ctx.set_store_policy(store, store)
     if args.occupancy is not None:
         ctx.set_occupancy(args.occupancy, args.occupancy)
@@ -281,7 +281,7 @@ def main() -> int:
         torch.cuda.synchronize()
         return 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
     ceil_shapes = {}
-    names = {-1: "default", 0: "plain", 1: "nt", 2: "sc1"}
+    names = {-1: "default", 0: "plain", 1: "nt", 2: "sc1", 3: "ntsc1"}
     for waves, occ, sp in [(args.waves_per_block or 2, -1 if args.occupancy is None else args.occupancy, store),
                            (4, 4, 2), (4, 3, 2), (2, 4, 2), (4, 0, 0), (4, 4, 0)]:
         ctx.set_waves_per_block(waves)
@@ -327,7 +327,8 @@ def main() -> int:
                        "bytes_per_step_all_ranks": int(total_bytes // args.steps),
                        "dedup": cfg["dedup"], "compress": list(cfg["compress"]) if isinstance(cfg["compress"], tuple) else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
-                       "stores": args.store if args.store != "default" else "sc1"},
+                       "stores": (args.store if args.store != "default"
+                                  else ("sc1" if cfg["size"] is None else "nt sc1"))},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic_from_profiles(args.config, int(sum(launch_bytes) / len(launch_bytes))),

@@ -30,7 +30,7 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 using namespace s3dg;
 
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
-constexpr int kDefaultStoreStream = kStoreSC1, kDefaultStoreBatch = kStoreSC1;
+constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
 // measured on MI355X (tools/k2_lab.py): 512-B row pieces and sc1 stores for
@@ -42,7 +42,8 @@ constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 2, 0, kStore
 struct s3dg_ctx {
     int device = 0;
     int cus = 256;                     // compute units (sizes small keystream launches)
-    // store cache policy: sc1 (write, then drop the line from L2) measured best
+    // store cache policy: sc1 (write, then drop the line from
+    // L2) for batches, nt sc1 for streams, measured best
     int store_stream = kDefaultStoreStream, store_batch = kDefaultStoreBatch;
     int waves_per_block = 0;           // 0 = auto: 2 for streams, 1 for batches (measured)
     // resident fill workgroups per CU (0 = hardware max); measured on MI355X
@@ -252,8 +253,8 @@ int s3dg_set_nontemporal(s3dg_ctx *c, int on) {
 
 int s3dg_set_store_policy(s3dg_ctx *c, int stream_policy, int batch_policy) {
     if (!c) return fail(S3DG_EINVAL, "null context");
-    if (stream_policy > kStoreSC1 || batch_policy > kStoreSC1)
-        return fail(S3DG_EINVAL, "store policy must be 0 (plain), 1 (nt), 2 (sc1) or negative (default)");
+    if (stream_policy > kStoreNTSC1 || batch_policy > kStoreNTSC1)
+        return fail(S3DG_EINVAL, "store policy must be 0 (plain), 1 (nt), 2 (sc1), 3 (nt sc1) or negative (default)");
     c->store_stream = stream_policy < 0 ? kDefaultStoreStream : stream_policy;
     c->store_batch = batch_policy < 0 ? kDefaultStoreBatch : batch_policy;
     return S3DG_OK;
@@ -283,7 +284,7 @@ int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wg
     if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(S3DG_EINVAL, "waves must be 1, 2 or 4");
     if (wgs_per_cu < 0 || wgs_per_cu > 40) return fail(S3DG_EINVAL, "workgroups per CU must be 0..40");
     if (min_lane_draws != 0 && min_lane_draws < 64) return fail(S3DG_EINVAL, "min_lane_draws must be >= 64");
-    if (store_policy > kStoreSC1) return fail(S3DG_EINVAL, "store policy must be 0, 1, 2 or negative");
+    if (store_policy > kStoreNTSC1) return fail(S3DG_EINVAL, "store policy must be 0, 1, 2, 3 or negative");
     std::lock_guard<std::mutex> g(c->mu);
     const KsShape &def = kDefaultKsShape[mode];
     c->ks[mode].draws = draws ? draws : def.draws;

@@ -53,10 +53,10 @@ struct TileRec {
 static_assert(sizeof(TileRec) == 64, "TileRec is one s_load_dwordx16");
 
 // store cache policy of the fill kernels (s3dg_set_store_policy)
-constexpr int kStorePlain = 0, kStoreNT = 1, kStoreSC1 = 2;
+constexpr int kStorePlain = 0, kStoreNT = 1, kStoreSC1 = 2, kStoreNTSC1 = 3;
 
 struct LaunchCfg {
-    int store;             // kStorePlain / kStoreNT / kStoreSC1
+    int store;             // kStorePlain / kStoreNT / kStoreSC1 / kStoreNTSC1
     int waves_per_block;   // 1, 2 or 4 wave64s per 4 KiB block (one workgroup)
     uint32_t dyn_lds = 0;  // reserved dynamic LDS per workgroup (occupancy cap)
     uint32_t prefetch_tiles = 0;   // batch: tile-record prefetch distance (0 = off)
@@ -101,7 +101,7 @@ struct KeystreamArgs {
 // store cache policy.
 struct KsShape {
     int draws, waves, wgs_per_cu;
-    int store;             // kStorePlain / kStoreNT / kStoreSC1
+    int store;             // kStorePlain / kStoreNT / kStoreSC1 / kStoreNTSC1
 };
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
                            const KsShape &sh, hipStream_t s);

@@ -80,11 +80,14 @@ struct Xoshiro {
 //   kStorePlain  global_store_dwordx4 (line kept in the XCD's L2)
 //   kStoreNT     ... nt  (__builtin_nontemporal_store)
 //   kStoreSC1    ... sc1 (line dropped from the L2 once written)
+//   kStoreNTSC1  ... nt sc1
 template <int SP>
 __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) {
     if constexpr (SP == kStoreNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
     else if constexpr (SP == kStoreSC1)
         asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (SP == kStoreNTSC1)
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
@@ -545,6 +548,8 @@ hipError_t launch_ks_one(uint8_t *dst, const KeystreamArgs &A, const uint64_t *j
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (store == kStoreSC1)
         hipLaunchKernelGGL((k_keystream<D, W, kStoreSC1>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+    else if (store == kStoreNTSC1)
+        hipLaunchKernelGGL((k_keystream<D, W, kStoreNTSC1>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
     else if (store == kStoreNT)
         hipLaunchKernelGGL((k_keystream<D, W, kStoreNT>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
     else
@@ -603,6 +608,7 @@ void launch_ceiling_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_
     do {                                                                        \
         if (lc.store == kStoreNT) S3DG_DISPATCH_W(kStoreNT, fn, lc, __VA_ARGS__);    \
         else if (lc.store == kStoreSC1) S3DG_DISPATCH_W(kStoreSC1, fn, lc, __VA_ARGS__); \
+        else if (lc.store == kStoreNTSC1) S3DG_DISPATCH_W(kStoreNTSC1, fn, lc, __VA_ARGS__); \
         else S3DG_DISPATCH_W(kStorePlain, fn, lc, __VA_ARGS__);                \
     } while (0)
 
@@ -627,6 +633,7 @@ hipError_t occ_one(bool batch, uint32_t lds, int *out) {
     do {                                                                        \
         if (lc.store == kStoreNT) S3DG_DISPATCH_RET_W(r, kStoreNT, fn, lc, __VA_ARGS__);    \
         else if (lc.store == kStoreSC1) S3DG_DISPATCH_RET_W(r, kStoreSC1, fn, lc, __VA_ARGS__); \
+        else if (lc.store == kStoreNTSC1) S3DG_DISPATCH_RET_W(r, kStoreNTSC1, fn, lc, __VA_ARGS__); \
         else S3DG_DISPATCH_RET_W(r, kStorePlain, fn, lc, __VA_ARGS__);         \
     } while (0)
 

@@ -142,7 +142,8 @@ class Context:
         call("s3dg_set_nontemporal", self._h, 1 if on else 0)
 
     def set_store_policy(self, stream_policy: int = -1, batch_policy: int = -1) -> None:
-        """Fill-kernel store cache policy: 0 plain, 1 nt, 2 sc1, -1 default; results are identical."""
+        """Fill-kernel store cache policy: 0 plain, 1 nt, 2 sc1, 3 nt sc1, -1 default;
+        results are identical."""
         call("s3dg_set_store_policy", self._h, int(stream_policy), int(batch_policy))
 
     def set_occupancy(self, stream_wgs_per_cu: int = -1, batch_wgs_per_cu: int = -1) -> None:

@@ -41,7 +41,7 @@ def _knobs(ctx, rnd):
     ctx.set_waves_per_block(rnd.choice([0, 1, 2, 4]))
     occ = rnd.choice([-1, 0, 4, 9, 14, 24])
     ctx.set_occupancy(occ, occ)
-    sp = rnd.choice([-1, 0, 1, 2])
+    sp = rnd.choice([-1, 0, 1, 2, 3])
     ctx.set_store_policy(sp, sp)
     ctx.set_batch_prefetch(rnd.choice([0, 1, 7, 128, 1 << 20]))
 
@@ -118,7 +118,7 @@ def test_fuzz_random_layout_keystream_dgen(gpu_ctx, torch, oracle, seed):
             for mode in (0, 1):
                 gpu_ctx.set_keystream_shape(mode, rnd.choice([0, 16, 32, 64]), rnd.choice([0, 1, 2, 4]),
                                             rnd.choice([0, 0, 1, 3]), rnd.choice([0, 64, 512, 4096]),
-                                            rnd.choice([-1, 0, 1, 2]))
+                                            rnd.choice([-1, 0, 1, 2, 3]))
             L = _size(rnd)
             chunk = rnd.choice([128, 1152, 65536, 2 << 20, (rnd.randint(1, 4096)) * 128])
             sb = rnd.getrandbits(64)

@@ -104,7 +104,7 @@ def test_stream_vs_oracle(gpu_ctx, torch, oracle, base, size, stride, n, d, c, f
 
 
 @pytest.mark.parametrize("waves,occ,pf,sp", [(1, -1, 128, -1), (2, -1, 128, 0), (4, -1, 128, 1), (1, 0, 0, 0),
-                                              (1, 20, 1, 1), (2, 12, 3, 2), (1, -1, 100000, -1)])
+                                              (1, 20, 1, 1), (2, 12, 3, 2), (1, -1, 100000, -1), (2, 14, 64, 3)])
 def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, pf, sp):
     gpu_ctx.set_waves_per_block(waves)
     gpu_ctx.set_occupancy(occ, occ)
@@ -152,7 +152,7 @@ def test_store_modes_and_occupancy_agree(gpu_ctx, torch):
     n, size = 40, 2**20 + 4096 * 3
     ref = torch.empty(n * size, dtype=torch.uint8, device="cuda")
     gpu_ctx.fill_stream(ref, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=5)
-    for sp in (-1, 0, 1, 2):
+    for sp in (-1, 0, 1, 2, 3):
         for waves in (1, 2, 4):
             for cap in (-1, 0, 3, 12, 40):
                 gpu_ctx.set_store_policy(sp, sp)

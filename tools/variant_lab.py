@@ -68,7 +68,7 @@ def main():
             off += (sz + 4095) // 4096 * 4096
         descs[kind] = (arr, sum(sizes))
     crcs = {}
-    work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
+    work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "stream5": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
             "cfg4": descs["cfg4"][1], "cfg7": descs["cfg7"][1]}
     buf = torch.empty(8 * MiB * n, dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
@@ -76,8 +76,8 @@ def main():
     p = ctypes.c_void_p(buf.data_ptr())
 
     def run(L, h, kind):
-        if kind in ("stream2", "stream3"):
-            d, fn, fd = (1, 0, 1) if kind == "stream2" else (4, 1, 2)
+        if kind in ("stream2", "stream3", "stream5"):
+            d, fn, fd = {"stream2": (1, 0, 1), "stream3": (4, 1, 2), "stream5": (2, 2, 3)}[kind]
             r = L.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(d), u32(fn), u32(fd),
                                               u64(SEED_BASE), u64(0), sh)
         elif kind == "ceiling":
