@@ -718,6 +718,7 @@ int dflt_init(DefaultCtx &D) {
 // the device base block.
 int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, const PrefixParams &pp, uint64_t entropy,
               const void *base) {
+    if (int r = check_ctx(D.ctx)) return r;     // the calling thread may have another device current
     const uint64_t nb = (len + kBlk - 1) / kBlk;
     const uint64_t cb = DefaultCtx::kChunk / kBlk;
     for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
@@ -824,6 +825,7 @@ int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, s
     if (int r = dflt_init(D)) return r;
     const void *base = D.ctx->base_dev;
     if (base4096) {
+        if (int r = check_ctx(D.ctx)) return r;
         HIP_TRY(hipMemcpy(D.base_user, base4096, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
         base = D.base_user;
     }

@@ -7,6 +7,7 @@
 #include "s3dlio_gpu.h"
 
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -19,6 +20,8 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 }  // namespace s3dg
 
 extern "C" int s3dg_internal_fail(int code, const char *msg);
+struct s3dg_ctx;
+extern "C" int s3dg_internal_ctx_device(s3dg_ctx *c, int *dev);
 
 namespace {
 
@@ -135,12 +138,29 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
     if (out_len < L.total) return s3dg_internal_fail(S3DG_EINVAL, "output buffer too small");
     uint32_t crc_x = crc32_host_update(0, L.hx.data(), L.hx.size());
     if (L.x_data) {
-        // cached grow-only device buffer + stream (one build at a time)
-        static std::mutex mu;
-        static void *dev = nullptr;
-        static uint64_t cap = 0;
-        static hipStream_t s = nullptr;
-        std::lock_guard<std::mutex> lk(mu);
+        // cached grow-only device buffer + stream per device (one build at a
+        // time per device)
+        struct Cache {
+            std::mutex mu;
+            void *dev = nullptr;
+            uint64_t cap = 0;
+            hipStream_t s = nullptr;
+        };
+        static std::mutex map_mu;
+        static std::map<int, Cache *> *caches = new std::map<int, Cache *>();   // never freed: outlives HIP
+        int device = 0;
+        if (int r = s3dg_internal_ctx_device(ctx, &device)) return r;
+        Cache *C;
+        {
+            std::lock_guard<std::mutex> g(map_mu);
+            Cache *&slot = (*caches)[device];
+            if (!slot) slot = new Cache();
+            C = slot;
+        }
+        std::lock_guard<std::mutex> lk(C->mu);
+        void *&dev = C->dev;
+        uint64_t &cap = C->cap;
+        hipStream_t &s = C->s;
         if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
             return s3dg_internal_fail(S3DG_EHIP, "hipStreamCreate");
         if (L.x_data > cap) {
