@@ -112,11 +112,12 @@ void base_from_seed(uint64_t seed, uint8_t *out) {
 
 constexpr uint64_t kDefaultBaseSeed = 0xBA5EB10C00000000ull;
 
-int check_ctx(s3dg_ctx *c) {
-    if (!c) return fail(S3DG_EINVAL, "null context");
-    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-    return S3DG_OK;
-}
+// Entry points: a null context is an error; the context's device is made
+// current for the call and the caller's current device restored afterwards.
+#define CTX_SCOPE(c)                                                   \
+    if (!(c)) return fail(S3DG_EINVAL, "null context");                \
+    DeviceScope dscope_((c)->device);                                  \
+    if (!dscope_.ok()) return hipfail(dscope_.err, "hipSetDevice")
 
 int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                 PrefixParams *pp) {
@@ -182,7 +183,8 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n), "hipGetDeviceCount");
     if (device < 0 || device >= n) return fail(S3DG_EINVAL, "device index out of range");
-    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    DeviceScope ds(device);
+    if (!ds.ok()) return hipfail(ds.err, "hipSetDevice");
     s3dg_ctx *c = new s3dg_ctx();
     c->device = device;
     int cus = 0;
@@ -201,7 +203,7 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
 
 int s3dg_ctx_destroy(s3dg_ctx *c) {
     if (!c) return S3DG_OK;
-    (void)hipSetDevice(c->device);
+    DeviceScope ds(c->device);
     (void)hipDeviceSynchronize();
     if (c->base_dev) (void)hipFree(c->base_dev);
     if (c->tab_dev) (void)hipFree(c->tab_dev);
@@ -216,7 +218,7 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
 }
 
 int s3dg_set_base_block(s3dg_ctx *c, const uint8_t *base) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!base) return fail(S3DG_EINVAL, "null base block");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");   // no launch may read the old block
@@ -296,14 +298,14 @@ int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wg
 }
 
 int s3dg_query_keystream_occupancy(s3dg_ctx *c, int mode, int *wgs_per_cu) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!wgs_per_cu || (mode != 0 && mode != 1)) return fail(S3DG_EINVAL, "bad argument");
     HIP_TRY(keystream_occupancy(c->ks[mode], wgs_per_cu), "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     return S3DG_OK;
 }
 
 int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!wgs_per_cu) return fail(S3DG_EINVAL, "null output");
     HIP_TRY(fill_occupancy(cfg_for(c, batch != 0), batch != 0, wgs_per_cu), "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     return S3DG_OK;
@@ -312,7 +314,7 @@ int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
 int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t blk_lo,
                                uint64_t blk_hi, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                                uint64_t entropy, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (len == 0) return S3DG_OK;                                   // :154-156
     const uint64_t nb = (len + kBlk - 1) / kBlk;
     if (blk_hi > nb) blk_hi = nb;
@@ -328,7 +330,7 @@ int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t bl
 }
 
 int s3dg_random_data(s3dg_ctx *c, void *dst, uint64_t len, uint64_t entropy, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (len == 0) return S3DG_OK;
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
     const uint64_t nb = (len + kBlk - 1) / kBlk;
@@ -344,8 +346,9 @@ int s3dg_random_data(s3dg_ctx *c, void *dst, uint64_t len, uint64_t entropy, voi
     return S3DG_OK;
 }
 
+// The context's device (callers make it current with a DeviceScope).
 int s3dg_internal_ctx_device(s3dg_ctx *c, int *dev) {
-    if (int r = check_ctx(c)) return r;
+    if (!c || !dev) return fail(S3DG_EINVAL, "null context");
     *dev = c->device;
     return S3DG_OK;
 }
@@ -357,7 +360,7 @@ int s3dg_internal_fill_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
                              uint64_t n_objs, uint64_t blk_lo, uint64_t blk_hi, int random_layout,
                              uint64_t dedup, uint32_t f_num, uint32_t f_den, uint64_t seed_base,
                              uint64_t first_obj, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (obj_size == 0 || n_objs == 0) return S3DG_OK;
     const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
     if (blk_hi > nb) blk_hi = nb;
@@ -387,7 +390,7 @@ int s3dg_fill_controlled(s3dg_ctx *c, void *dst, uint64_t len, uint64_t dedup, u
 int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride,
                                 uint64_t n_objs, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                                 uint64_t seed_base, uint64_t first_obj, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (obj_size == 0 || n_objs == 0) return S3DG_OK;
     if (!dst || !aligned16(dst) || (stride & 15u))
         return fail(S3DG_EINVAL, "dst and stride must be 16-byte aligned");
@@ -404,7 +407,7 @@ int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint6
 
 int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc *d, uint64_t n,
                                void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (n == 0) return S3DG_OK;
     if (!d) return fail(S3DG_EINVAL, "null descriptor array");
     if (!dst_base || !aligned16(dst_base)) return fail(S3DG_EINVAL, "dst_base must be 16-byte aligned");
@@ -504,7 +507,7 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
 
 int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes,
                       uint64_t seed_base, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (len == 0) return S3DG_OK;
     if (chunk_bytes == 0 || (chunk_bytes & 127u))
         return fail(S3DG_EINVAL, "chunk_bytes must be a positive multiple of 128");
@@ -541,7 +544,7 @@ int s3dg_dgen_fill(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t blk_lo, u
 int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride, uint64_t n_objs,
                              uint64_t blk_lo, uint64_t blk_hi, uint64_t dedup, uint32_t f_num,
                              uint32_t f_den, uint64_t seed_base, uint64_t first_obj, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (obj_size == 0 || n_objs == 0) return S3DG_OK;
     const uint64_t nb = (obj_size + kDgenBlock - 1) / kDgenBlock;
     if (blk_hi > nb) blk_hi = nb;
@@ -573,7 +576,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
 }
 
 int s3dg_crc32(s3dg_ctx *c, const void *dev, uint64_t len, void *stream, uint32_t *out) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!out || (len && !dev)) return fail(S3DG_EINVAL, "null argument");
     if (len && !aligned16(dev)) return fail(S3DG_EINVAL, "dev must be 16-byte aligned");
     std::lock_guard<std::mutex> g(c->crc_mu);
@@ -596,7 +599,7 @@ uint32_t s3dg_crc32_host(uint32_t crc, const uint8_t *p, uint64_t n) {
 }
 
 int s3dg_write_ceiling(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!dst || !aligned16(dst) || (len % kBlk))
         return fail(S3DG_EINVAL, "dst must be 16-byte aligned and len a multiple of 4096");
     HIP_TRY(launch_write_ceiling(cfg_for(c), (uint8_t *)dst, len, pattern, (hipStream_t)stream),
@@ -605,14 +608,14 @@ int s3dg_write_ceiling(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, v
 }
 
 int s3dg_device_alloc(s3dg_ctx *c, uint64_t bytes, void **out) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!out) return fail(S3DG_EINVAL, "null output");
     HIP_TRY(hipMalloc(out, bytes), "hipMalloc");
     return S3DG_OK;
 }
 
 int s3dg_device_free(s3dg_ctx *c, void *p) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     HIP_TRY(hipFree(p), "hipFree");
     return S3DG_OK;
 }
@@ -629,21 +632,21 @@ int s3dg_host_free_pinned(void *p) {
 }
 
 int s3dg_d2h_async(s3dg_ctx *c, void *host, const void *dev, uint64_t len, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     HIP_TRY(hipMemcpyAsync(host, dev, len, hipMemcpyDeviceToHost, (hipStream_t)stream),
             "hipMemcpyAsync(D2H)");
     return S3DG_OK;
 }
 
 int s3dg_h2d_async(s3dg_ctx *c, void *dev, const void *host, uint64_t len, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     HIP_TRY(hipMemcpyAsync(dev, host, len, hipMemcpyHostToDevice, (hipStream_t)stream),
             "hipMemcpyAsync(H2D)");
     return S3DG_OK;
 }
 
 int s3dg_stream_create(s3dg_ctx *c, void **out) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (!out) return fail(S3DG_EINVAL, "null output");
     hipStream_t s;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
@@ -652,13 +655,13 @@ int s3dg_stream_create(s3dg_ctx *c, void **out) {
 }
 
 int s3dg_stream_destroy(s3dg_ctx *c, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     HIP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
     return S3DG_OK;
 }
 
 int s3dg_sync(s3dg_ctx *c, void *stream) {
-    if (int r = check_ctx(c)) return r;
+    CTX_SCOPE(c);
     if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
     else HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     return S3DG_OK;
@@ -718,7 +721,7 @@ int dflt_init(DefaultCtx &D) {
 // the device base block.
 int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, const PrefixParams &pp, uint64_t entropy,
               const void *base) {
-    if (int r = check_ctx(D.ctx)) return r;     // the calling thread may have another device current
+    CTX_SCOPE(D.ctx);     // the calling thread may have another device current
     const uint64_t nb = (len + kBlk - 1) / kBlk;
     const uint64_t cb = DefaultCtx::kChunk / kBlk;
     for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
@@ -825,7 +828,7 @@ int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, s
     if (int r = dflt_init(D)) return r;
     const void *base = D.ctx->base_dev;
     if (base4096) {
-        if (int r = check_ctx(D.ctx)) return r;
+        CTX_SCOPE(D.ctx);
         HIP_TRY(hipMemcpy(D.base_user, base4096, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
         base = D.base_user;
     }

@@ -26,7 +26,7 @@
 
 extern "C" int s3dg_internal_fail(int code, const char *msg);   // s3dg_capi.cpp
 extern "C" s3dg_ctx *s3dg_internal_default_ctx(int *err);       // s3dg_capi.cpp
-extern "C" int s3dg_internal_ctx_device(s3dg_ctx *c, int *dev);  // s3dg_capi.cpp (sets it current)
+extern "C" int s3dg_internal_ctx_device(s3dg_ctx *c, int *dev);  // s3dg_capi.cpp
 
 // Device staging for host-buffer generation: two 64 MiB chunks + two
 // streams.  Pooled process-wide so short-lived generators (generate_data on
@@ -112,6 +112,8 @@ int fill_range(s3dg_gen *g, uint8_t *buf, uint64_t pos, uint64_t n) {
     // allocated (and kernels launched) on the context's device
     int dev = 0;
     if (int r = s3dg_internal_ctx_device(g->ctx, &dev)) return r;
+    DeviceScope ds(dev);
+    if (!ds.ok()) return s3dg_internal_fail(S3DG_EHIP, "hipSetDevice");
     if (int r = acquire_scratch(g)) return r;
     Scratch *sc = g->sc;
     const uint64_t b0 = pos / kDgenBlock, b1 = (pos + n + kDgenBlock - 1) / kDgenBlock;

@@ -145,4 +145,23 @@ private:
     bool active_ = false;
 };
 
+// Makes `device` current for the scope and restores the caller's current
+// device afterwards, so a C-ABI call never changes the calling thread's HIP
+// (and torch's) current device.
+struct DeviceScope {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) err = hipSetDevice(device);
+        else prev = -1;                                  // nothing to restore
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    bool ok() const { return err == hipSuccess; }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 }  // namespace s3dg

@@ -150,6 +150,8 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
         static std::map<int, Cache *> *caches = new std::map<int, Cache *>();   // never freed: outlives HIP
         int device = 0;
         if (int r = s3dg_internal_ctx_device(ctx, &device)) return r;
+        DeviceScope ds(device);
+        if (!ds.ok()) return s3dg_internal_fail(S3DG_EHIP, "hipSetDevice");
         Cache *C;
         {
             std::lock_guard<std::mutex> g(map_mu);

@@ -493,6 +493,7 @@ extern "C" int s3dg_put_objects_multi(s3dg_ctx *const *ctxs, uint32_t nctx, cons
     }
     for (uint32_t k = 0; k < L; ++k) {
         locks.emplace_back(pools[k]->mu);
+        DeviceScope ds(devs[k]);
         if (int r = pool_init(*pools[k], devs[k])) return r;
     }
 
@@ -530,7 +531,8 @@ extern "C" int s3dg_put_objects_multi(s3dg_ctx *const *ctxs, uint32_t nctx, cons
         std::vector<std::string> lerr(L);
         auto lane_main = [&](uint32_t k) {
             NumaScope numa(devs[k]);
-            if (hipSetDevice(devs[k]) != hipSuccess) {
+            DeviceScope ds(devs[k]);
+            if (!ds.ok()) {
                 lrc[k] = s3dg_internal_fail(S3DG_EHIP, "hipSetDevice");
             } else {
                 const uint64_t q = n / L, r = n % L;
