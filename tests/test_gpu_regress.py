@@ -40,3 +40,48 @@ def test_batch_growth_keeps_cached_tables(oracle):
         ctx.sync()
         check()                                       # the cached tables must still be valid
     del ctx
+
+
+@pytest.mark.gpu
+def test_no_device_or_host_leak_across_repeated_calls(tmp_path):
+    """Repeated generate_data / generate_npz_bytes / Generator / contexts /
+    put_objects / batches must not grow device memory or pinned host memory:
+    every cache is bounded and every context frees what it allocated."""
+    import gc
+    import resource
+    import torch
+    import s3dlio_amd as S
+
+    def dev_used():
+        torch.cuda.synchronize()
+        free, total = torch.cuda.mem_get_info()
+        return total - free
+
+    def round_():
+        for _ in range(20):
+            assert len(S.generate_data(3 << 20, 2, 2)) == 3 << 20
+        S.generate_npz_bytes([256, 256, 3])
+        for _ in range(20):
+            g = S.Generator(5 << 20, 1, 3, seed=1)
+            b = bytearray(1 << 20)
+            while g.fill_chunk(b):
+                pass
+        for _ in range(5):
+            with S.Context(0) as c:
+                t = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+                c.fill_batch(t, [(0, 4096 * 3 + 7, 1, 2, 3), (16384, 100000, 2, 1, 1)])
+                c.xoshiro_fill(t, 1 << 20)
+                c.sync()
+                del t
+        S.put_objects([f"file://{tmp_path}/o{j}" for j in range(8)], 70000, seed=3)
+        gc.collect()
+
+    round_()                                   # first use creates the bounded caches
+    d0 = dev_used()
+    r0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    for _ in range(3):
+        round_()
+    d1 = dev_used()
+    r1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    assert d1 - d0 < 64 << 20, (d0, d1)        # device memory flat (allocator noise only)
+    assert (r1 - r0) * 1024 < 512 << 20, (r0, r1)
