@@ -99,3 +99,27 @@ def test_batch_config4_every_byte(env):
             assert _compare(torch, host, chk, dev[w0:w1], w1 - w0), (j, k)
             j = k
     del dev
+
+
+def test_keystream_config6_every_byte(env):
+    """bench.py --config 6: 10 000 x 8 MiB written as 2 MiB Xoshiro256++ chunks
+    (the npz x-fill, src/data_formats/npz.rs:376-383), chunk k seeded k."""
+    torch, S, OC, ctx, base, host, chk = env
+    total, chunk = 10000 * 8 * MiB, 2 * MiB
+    dev = torch.empty(total, dtype=torch.uint8, device="cuda")
+    ctx.xoshiro_fill(dev, total, chunk_bytes=chunk, seed_base=0)
+    torch.cuda.synchronize()
+    lib = OC.lib()
+    hbase = host.data_ptr()
+    per_task = 64 * chunk
+
+    def one(args):
+        off, k0, n = args
+        lib.s3dgo_xoshiro_chunks(ctypes.cast(hbase + off, ctypes.POINTER(ctypes.c_uint8)), n, chunk, k0)
+    with cf.ThreadPoolExecutor(THREADS) as pool:
+        for w0 in range(0, total, WINDOW):
+            n = min(WINDOW, total - w0)
+            tasks = [(o, (w0 + o) // chunk, min(per_task, n - o)) for o in range(0, n, per_task)]
+            list(pool.map(one, tasks))
+            assert _compare(torch, host, chk, dev[w0:w0 + n], n), w0
+    del dev
