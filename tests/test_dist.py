@@ -40,7 +40,7 @@ def _worker(rank, world, port, n_total, size, q):
     cp.close()
 
 
-@pytest.mark.parametrize("n_total,world", [(7, 2), (64, 2)])
+@pytest.mark.parametrize("n_total,world", [(7, 2), (64, 2), (37, 4)])
 def test_two_rank_sharding_matches_single_stream(oracle, n_total, world):
     size = 4096 * 3 + 100
     ctx = mp.get_context("spawn")
@@ -78,3 +78,18 @@ def test_entropy_independent_of_world_size(oracle):
     a = oracle.fill_stream(8192, 6, 1, 0, 1, SEED_BASE, 0, base)
     b = np.concatenate([oracle.fill_stream(8192, 2, 1, 0, 1, SEED_BASE, k, base) for k in (0, 2, 4)])
     assert np.array_equal(a, b)
+
+
+def test_bench_config_math():
+    """bench.py's config 4 sizes follow SURVEY.md §8d (log-uniform 4 KiB..64 MiB,
+    SplitMix64(seed 4), mean (b-a)/ln(b/a) ~= 6.9 MB) and config 5 splits
+    100 000 objects over 8 ranks as 12 500 each."""
+    import math
+    import bench
+    s = bench.log_uniform_sizes(10000)
+    assert min(s) >= 4096 and max(s) <= 64 << 20
+    mean = (64 * 2**20 - 4096) / math.log(64 * 2**20 / 4096)
+    assert abs(sum(s) / len(s) - mean) / mean < 0.05
+    assert s == bench.log_uniform_sizes(10000)                  # deterministic
+    assert sum(s) == 68647437822                                 # the bytes bench.py and the profiles report
+    assert [object_range(100000, r, 8) for r in (0, 7)] == [(0, 12500), (87500, 100000)]
