@@ -81,6 +81,9 @@ int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_c
 /* Batch launches: distance (in 64-block tiles) at which workgroups warm the
  * L2 with a later tile record; 0 = off.  Default 128.  Results are identical. */
 int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
+/* Batch launches: blocks per tile record (8, 16, 32 or 64); 0 = chosen per
+ * launch from the object sizes (default).  Results are identical. */
+int s3dg_set_batch_tile(s3dg_ctx *ctx, uint32_t blocks);
 /* Keystream kernel launch shape for mode 0 (npz keystream, s3dg_xoshiro_fill)
  * or mode 1 (DG1, s3dg_dgen_fill and the generators): draws staged per lane
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident

@@ -50,6 +50,7 @@ struct s3dg_ctx {
     // (DESIGN.md §5.1): 14 for 2-wave stream blocks, no cap for 1-wave batch blocks
     int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
     uint32_t prefetch_tiles = 128;     // batch tile-record prefetch distance
+    uint32_t tile_shift = 0;           // batch tile = 2^tile_shift blocks; 0 = per launch
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
     uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
@@ -145,6 +146,25 @@ LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false) {
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Batch tile size: every object's last tile is ragged, and its blocks past
+// the object's end are workgroups that start, load the record and exit.
+// Smaller tiles cut those, at one 64-B record (and one more record miss per
+// XCD) per tile.  Pick the tile size that minimises launched workgroups +
+// kTileCost x records.
+constexpr uint64_t kTileCost = 2;
+#ifndef S3DG_XCD_ALIGN
+#define S3DG_XCD_ALIGN 1
+#endif
+uint32_t pick_tile_shift(const uint64_t (&ntiles)[kTileShiftMax + 1]) {
+    uint32_t best = kTileShiftMax;
+    uint64_t best_cost = UINT64_MAX;
+    for (uint32_t sh = kTileShiftMax; sh >= kTileShiftMin; --sh) {
+        const uint64_t cost = (ntiles[sh] << sh) + kTileCost * ntiles[sh];
+        if (cost < best_cost) { best_cost = cost; best = sh; }
+    }
+    return best;
+}
 
 }  // namespace
 
@@ -274,6 +294,18 @@ int s3dg_set_occupancy(s3dg_ctx *c, int stream_wgs_per_cu, int batch_wgs_per_cu)
 int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
     if (!c) return fail(S3DG_EINVAL, "null context");
     c->prefetch_tiles = tiles;
+    return S3DG_OK;
+}
+
+int s3dg_set_batch_tile(s3dg_ctx *c, uint32_t blocks) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    uint32_t sh = 0;
+    if (blocks != 0) {
+        while ((1u << sh) < blocks) ++sh;
+        if ((1u << sh) != blocks || sh < kTileShiftMin || sh > kTileShiftMax)
+            return fail(S3DG_EINVAL, "tile blocks must be 0 (per launch), 8, 16, 32 or 64");
+    }
+    c->tile_shift = sh;
     return S3DG_OK;
 }
 
@@ -424,9 +456,9 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
                 "hipHostMalloc(batch table)");
         c->tab_cap = cap;
     }
-    // Objects of size 0 contribute no tiles; the search skips them because
-    // the next entry has the same tile_begin.
-    uint64_t tiles = 0, m = 0;
+    // Objects of size 0 contribute no tiles and no table entry.
+    uint64_t m = 0;
+    uint64_t ntiles[kTileShiftMax + 1] = {};
     for (uint64_t k = 0; k < n; ++k) {
         if (d[k].size == 0) continue;
         if (d[k].dst_off & 15u) return fail(S3DG_EINVAL, "dst_off must be a multiple of 16");
@@ -435,11 +467,22 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         e.dst_off = d[k].dst_off;
         e.size = d[k].size;
         e.entropy = d[k].entropy;
-        e.tile_begin = tiles;
+        // XCD alignment: slot (mod 8) = 4 KiB granule (mod 8) of the block's address
+        e.lead = S3DG_XCD_ALIGN ? (uint32_t)((((uintptr_t)dst_base + d[k].dst_off) >> 12) & 7) : 0;
+        e.pad = 0;
+        e.tile_begin = nb + e.lead;   // slot count until the tile size is known
         if (int r = make_prefix(nb, d[k].dedup, d[k].f_num, d[k].f_den, &e.pp)) return r;
-        tiles += (nb + kTileBlocks - 1) / kTileBlocks;
+        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
+            ntiles[sh] += (nb + e.lead + (1ull << sh) - 1) >> sh;
     }
     if (m == 0) return S3DG_OK;
+    const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
+    uint64_t tiles = 0;
+    for (uint64_t k = 0; k < m; ++k) {
+        const uint64_t slots = c->tab_host[k].tile_begin;
+        c->tab_host[k].tile_begin = tiles;
+        tiles += (slots + (1ull << tshift) - 1) >> tshift;
+    }
     if (tiles > c->tile_cap) {
         // the previous batch may still read the old map: it is stream-ordered
         // only on its own stream, so drain the device before freeing
@@ -454,7 +497,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     HIP_TRY(hipMemcpyAsync(c->tab_dev, c->tab_host, m * sizeof(ObjEntry), hipMemcpyHostToDevice, s),
             "hipMemcpyAsync(batch table)");
     HIP_TRY(hipEventRecord(c->tab_free, s), "hipEventRecord");
-    HIP_TRY(launch_fill_batch(cfg_for(c, true), (uint8_t *)dst_base, c->tab_dev, m, tiles,
+    HIP_TRY(launch_fill_batch(cfg_for(c, true), (uint8_t *)dst_base, c->tab_dev, m, tiles, tshift,
                               c->tile_obj, c->base_dev, s),
             "launch k_fill_batch");
     return S3DG_OK;

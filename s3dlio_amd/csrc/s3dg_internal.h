@@ -12,7 +12,9 @@ constexpr uint32_t kBlk = 4096;   // BLK_SIZE   src/constants.rs:326
 constexpr uint32_t kHalf = 2048;  // HALF_BLK   src/constants.rs:329
 constexpr uint32_t kMod = 32;     // MOD_SIZE   src/constants.rs:352
 constexpr uint64_t kDgenBlock = 1ull << 20;   // DGEN_BLOCK_SIZE src/constants.rs:348
-constexpr uint32_t kTileBlocks = 64;  // blocks per batch tile (tile -> object map granule)
+// batch tiles (tile -> object map granule) are 2^tshift blocks, tshift in
+// [kTileShiftMin, kTileShiftMax], chosen per launch (s3dg_capi.cpp pick_tile_shift)
+constexpr uint32_t kTileShiftMin = 3, kTileShiftMax = 6;
 constexpr int kWavesPerWG = 4;
 
 // Zero-prefix parameters of one object: const_len(u) =
@@ -36,18 +38,20 @@ struct ObjEntry {
     uint64_t dst_off;
     uint64_t size;
     uint64_t entropy;
-    uint64_t tile_begin;   // exclusive prefix sum of ceil(nblocks/64)
+    uint64_t tile_begin;   // exclusive prefix sum of tiles per object
     PrefixParams pp;
+    uint32_t lead;         // dead slots before block 0 in the first tile (XCD alignment)
+    uint32_t pad;
 };
 
 // One 64-block tile of a batch object, written by k_tile_map so the fill
 // kernel reaches everything with a single 64-byte scalar load.
 struct TileRec {
-    uint64_t dst_off;      // byte offset of the tile's first block
+    uint64_t dst_off;      // byte offset of the object
     uint64_t size;         // object size
     uint64_t entropy;
-    uint32_t first;        // first block index of the tile within the object
-    uint32_t pad;
+    uint32_t first;        // first slot of the tile: tile index x tile blocks
+    uint32_t lead;         // slot of block 0: block = first + slot - lead
     PrefixParams pp;
 };
 static_assert(sizeof(TileRec) == 64, "TileRec is one s_load_dwordx16");
@@ -74,7 +78,7 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               PrefixParams pp, const void *base_dev, hipStream_t s);
 
 hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, TileRec *tiles,
+                             uint64_t n, uint64_t total_tiles, uint32_t tshift, TileRec *tiles,
                              const void *base_dev, hipStream_t s);
 
 // K2 keystream launch: chunks [chunk0, chunk0 + nchunks) of an obj_len-byte

@@ -292,21 +292,27 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t 
                       seed_base + ((first_obj + j) << 32), pp, B);
 }
 
-// Batch: workgroup g -> tile record g/64 (one scalar load), block
-// first + (g % 64) of that object; blocks past the object's end exit.
-// pf > 0: the first 8 workgroups of a tile (one per XCD: workgroups are dealt
-// round-robin to the XCDs) load the record of tile + pf after their stores,
-// result unused, so it is in that XCD's L2 when its workgroups start.  pf must
-// exceed the tiles in flight (resident workgroups / 64); see DESIGN.md §5.1.
+// Batch: workgroup g -> tile record g >> tshift (one scalar load), block
+// first + (g mod 2^tshift) - lead of that object; slots before the object's
+// start (lead) or past its end exit.  lead makes g = 4 KiB-granule address
+// (mod 8), as in the stream kernel: workgroups are dealt round-robin to the
+// 8 XCDs, so XCD x writes only granules = x (mod 8).
+// Tiles are 2^tshift blocks (8..64, chosen per launch by the host so the
+// dead workgroups of ragged object tails stay few).
+// pf > 0: the first 8 workgroups of every 256 blocks (one per XCD: workgroups
+// are dealt round-robin to the XCDs) touch the records of the 256 blocks
+// 64*pf blocks ahead (one lane per 128-byte line of records) after their
+// stores, result unused, so they are in that XCD's L2 when its workgroups
+// start.  pf must exceed the resident workgroups / 64.
 template <int NT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
-                                                        const u32x4 *base) {
+                                                        uint32_t tshift, const u32x4 *base) {
     __shared__ __attribute__((aligned(16))) BlockLds S;
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const uint64_t g = g0 + blockIdx.x;
-    const uint64_t tile = g >> 6;
+    const uint64_t tile = g >> tshift;
     // The tile record (64 B) in ONE scalar load, issued first; then the base
     // block's vector loads and its LDS image, so the two memory latencies
     // overlap instead of following each other (the compiler otherwise splits
@@ -319,32 +325,40 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     // the wait "redefines" raw, so no use of the record can move above it
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(raw) :: "memory");
     const TileRec e = __builtin_bit_cast(TileRec, raw);
-    const uint32_t k = (uint32_t)(g & 63);
-    const uint64_t ib = (uint64_t)e.first + k;
-    if (ib * kBlk >= e.size) return;               // uniform for the whole workgroup
-    gen_block<NT, NW, true>(dst_base + e.dst_off + (uint64_t)k * kBlk, S, t, wave, (uint32_t)ib, e.size,
+    const uint32_t k = (uint32_t)(g & ((1u << tshift) - 1));
+    const int64_t ib = (int64_t)e.first + k - e.lead;
+    if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
+    gen_block<NT, NW, true>(dst_base + e.dst_off + (uint64_t)ib * kBlk, S, t, wave, (uint32_t)ib, e.size,
                             e.entropy, e.pp, B);
-    if (pf && k < 8 && t == 0) {
-        const uint64_t pt = tile + pf;
+#ifndef S3DG_PF_SPAN
+#define S3DG_PF_SPAN 256
+#endif
+    // one prefetching workgroup per XCD per span blocks; lane q of it
+    // touches the q-th 128-byte line (2 records) of the span's records
+    const uint32_t span = (uint32_t)S3DG_PF_SPAN > (2u << tshift) ? (uint32_t)S3DG_PF_SPAN : (2u << tshift);
+    if (pf && (g & (span - 1)) < 8 && t < (span >> (tshift + 1))) {
+        const uint64_t pt = (((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift) + 2 * t;
         const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
         uint32_t dummy;
         asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
     }
 }
 
-// tiles[tile] = record of every 64-block tile of every object.
-__global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t n, TileRec *tiles) {
+// tiles[tile] = record of every 2^tshift-block tile of every object.
+__global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t n, TileRec *tiles,
+                                                  uint32_t tshift) {
     const uint64_t k = blockIdx.x;
     if (k >= n) return;
     const ObjEntry e = tab[k];
-    const uint64_t nt = ((e.size + kBlk - 1) / kBlk + kTileBlocks - 1) / kTileBlocks;
+    const uint64_t tb = 1ull << tshift;
+    const uint64_t nt = ((e.size + kBlk - 1) / kBlk + e.lead + tb - 1) >> tshift;
     for (uint64_t q = threadIdx.x; q < nt; q += blockDim.x) {
         TileRec r;
-        r.dst_off = e.dst_off + q * kTileBlocks * kBlk;
+        r.dst_off = e.dst_off;
         r.size = e.size;
         r.entropy = e.entropy;
-        r.first = (uint32_t)(q * kTileBlocks);
-        r.pad = 0;
+        r.first = (uint32_t)(q * tb);
+        r.lead = e.lead;
         r.pp = e.pp;
         tiles[e.tile_begin + q] = r;
     }
@@ -588,8 +602,8 @@ void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t
 
 template <int NT, int NW>
 void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
-                      uint64_t ntiles, uint64_t g0, uint32_t pf, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, b);
+                      uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b);
 }
 
 template <int NT, int NW>
@@ -673,18 +687,18 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
 }
 
 hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, TileRec *tiles,
+                             uint64_t n, uint64_t total_tiles, uint32_t tshift, TileRec *tiles,
                              const void *base_dev, hipStream_t s) {
     (void)hipGetLastError();
-    hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tiles);
+    hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tiles, tshift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
-    const uint64_t total = total_tiles * kTileBlocks;
+    const uint64_t total = total_tiles << tshift;
     for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
         S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
-                      lc.prefetch_tiles, b);
+                      lc.prefetch_tiles, tshift, b);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -155,6 +155,11 @@ class Context:
         """Tile-record prefetch distance of batch launches (0 = off); results are identical."""
         call("s3dg_set_batch_prefetch", self._h, int(tiles))
 
+    def set_batch_tile(self, blocks: int = 0) -> None:
+        """Blocks per batch tile record: 8, 16, 32, 64, or 0 = chosen per launch;
+        results are identical."""
+        call("s3dg_set_batch_tile", self._h, int(blocks))
+
     def set_keystream_shape(self, mode: int, draws: int = 0, waves: int = 0, wgs_per_cu: int = 0,
                             min_lane_draws: int = 0, store_policy: int = -1) -> None:
         """k_keystream launch shape for mode 0 (npz keystream) or 1 (DG1);

@@ -4,7 +4,7 @@ bytes around every output.  Complements the fixed edge-case fixtures: random
 sizes (ragged tails, 1..7-byte tails, block and chunk boundaries), dedup
 factors, integer and rational compress ratios, entropies near 2^64, random
 base blocks and random launch knobs (waves, occupancy, store policy,
-prefetch, keystream shape).  Reference semantics: src/data_gen.rs:151-224
+prefetch, batch tile size, keystream shape).  Reference semantics: src/data_gen.rs:151-224
 (fill), :102-132 (random-data layout), src/data_formats/npz.rs:376-383 (K2).
 """
 import random
@@ -44,6 +44,7 @@ def _knobs(ctx, rnd):
     sp = rnd.choice([-1, 0, 1, 2, 3])
     ctx.set_store_policy(sp, sp)
     ctx.set_batch_prefetch(rnd.choice([0, 1, 7, 128, 1 << 20]))
+    ctx.set_batch_tile(rnd.choice([0, 0, 8, 16, 32, 64]))
 
 
 def _reset(ctx):
@@ -51,6 +52,7 @@ def _reset(ctx):
     ctx.set_occupancy(-1, -1)
     ctx.set_store_policy(-1, -1)
     ctx.set_batch_prefetch(128)
+    ctx.set_batch_tile(0)
     ctx.set_keystream_shape(0)
     ctx.set_keystream_shape(1)
 

@@ -103,13 +103,15 @@ def test_stream_vs_oracle(gpu_ctx, torch, oracle, base, size, stride, n, d, c, f
     assert (got[stride * n:] == GUARD).all()
 
 
-@pytest.mark.parametrize("waves,occ,pf,sp", [(1, -1, 128, -1), (2, -1, 128, 0), (4, -1, 128, 1), (1, 0, 0, 0),
-                                              (1, 20, 1, 1), (2, 12, 3, 2), (1, -1, 100000, -1), (2, 14, 64, 3)])
-def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, pf, sp):
+@pytest.mark.parametrize("waves,occ,pf,sp,tile", [
+    (1, -1, 128, -1, 0), (2, -1, 128, 0, 64), (4, -1, 128, 1, 8), (1, 0, 0, 0, 16), (1, 20, 1, 1, 32),
+    (2, 12, 3, 2, 8), (1, -1, 100000, -1, 64), (2, 14, 64, 3, 0), (1, -1, 128, -1, 8), (1, 26, 0, -1, 16)])
+def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, pf, sp, tile):
     gpu_ctx.set_waves_per_block(waves)
     gpu_ctx.set_occupancy(occ, occ)
     gpu_ctx.set_batch_prefetch(pf)
     gpu_ctx.set_store_policy(sp, sp)
+    gpu_ctx.set_batch_tile(tile)
     rnd = random.Random(7)
     sizes = [0, 1, 5, 31, 32, 33, 4095, 4096, 4097, 2**20 + 3, 3 * 2**20, 65536 * 64 + 11]
     sizes += [int(np.exp(rnd.uniform(np.log(4096), np.log(4 * 2**20)))) for _ in range(40)]
@@ -133,6 +135,7 @@ def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, p
     gpu_ctx.set_occupancy(-1, -1)
     gpu_ctx.set_batch_prefetch(128)
     gpu_ctx.set_store_policy(-1, -1)
+    gpu_ctx.set_batch_tile(0)
 
 
 def test_range_pieces_compose(gpu_ctx, torch, oracle, base):
@@ -259,6 +262,9 @@ def test_invalid_arguments_raise(gpu_ctx, torch):
         gpu_ctx.fill_controlled(int(t.data_ptr()) + 1, 100)
     with pytest.raises(ValueError):
         gpu_ctx.fill_stream(t, obj_size=4096, n_objs=2, stride=100)
+    for bad in (1, 4, 9, 128):
+        with pytest.raises(ValueError, match="tile"):
+            gpu_ctx.set_batch_tile(bad)
 
 
 def test_keystream_golden_fixtures(gpu_ctx, torch):

@@ -2,9 +2,10 @@
 """Diagnostic: A/B of compile-time kernel variants on the same workloads,
 interleaved in one process.  Each variant is the product library built with
 extra -D flags (LAB_VARIANTS="name=-DFOO=1 -DBAR=2;name2=").  Points as in
-tools/batch_lab.py: "kind:waves:occ:pf:store;..." with kind in
+tools/batch_lab.py: "kind:waves:occ:pf:store[:tile];..." with kind in
 stream2 (cfg2 stream), stream3 (cfg3 stream), cfg4 (log-uniform batch),
-cfg7 (uniform 8 MiB batch), ceiling (store-only kernel), crc (s3dg_crc32).
+cfg7 (uniform 8 MiB batch), small (log-uniform 4 KiB-1 MiB batch), mid
+(uniform 1 MiB + 123 B batch), ceiling (store-only kernel), crc (s3dg_crc32).
 
     LAB_VARIANTS=... python tools/variant_lab.py --build-only   # here
     LAB_VARIANTS=... LAB_POINTS=... python tools/variant_lab.py # GPU box
@@ -60,17 +61,21 @@ def main():
         assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
         libs[name] = (L, h)
     descs = {}
-    for kind, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3), ("cfg7", [8 * MiB] * n, 1, 0, 1)]:
-        arr = (ObjDesc * n)()
+    for kind, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3), ("cfg7", [8 * MiB] * n, 1, 0, 1),
+                                   ("small", log_uniform_sizes(10 * n, 5, 4096, MiB), 1, 0, 1),
+                                   ("mid", [MiB + 123] * (5 * n), 3, 2, 3),
+                                   ("kb64", [64 << 10] * (10 * n), 1, 0, 1),
+                                   ("kb20", [(20 << 10) + 5] * (20 * n), 1, 0, 1)]:
+        arr = (ObjDesc * len(sizes))()
         off = 0
         for j, sz in enumerate(sizes):
             arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), d, fn, fd)
             off += (sz + 4095) // 4096 * 4096
-        descs[kind] = (arr, sum(sizes))
+        descs[kind] = (arr, sum(sizes), off)
     crcs = {}
     work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "stream5": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
-            "cfg4": descs["cfg4"][1], "cfg7": descs["cfg7"][1]}
-    buf = torch.empty(8 * MiB * n, dtype=torch.uint8, device="cuda")
+            **{k: v[1] for k, v in descs.items()}}
+    buf = torch.empty(max([8 * MiB * n] + [v[2] for v in descs.values()]), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     sh = ctypes.c_void_p(st.cuda_stream)
     p = ctypes.c_void_p(buf.data_ptr())
@@ -87,21 +92,22 @@ def main():
             r = L.s3dg_crc32(h, p, u64(8 * MiB * n), sh, ctypes.byref(out))
             crcs.setdefault(L, set()).add(out.value)
         else:
-            r = L.s3dg_fill_controlled_batch(h, p, descs[kind][0], u64(n), sh)
+            r = L.s3dg_fill_controlled_batch(h, p, descs[kind][0], u64(len(descs[kind][0])), sh)
         assert r == 0
     pts = []
     for item in os.environ.get("LAB_POINTS", "stream2:2:-1:128:-1;cfg4:1:-1:128:-1").split(";"):
-        k, w, o, f, sp = item.split(":")
-        pts.append((k, int(w), int(o), int(f), int(sp)))
+        k, w, o, f, sp, *tb = item.split(":")
+        pts.append((k, int(w), int(o), int(f), int(sp), int(tb[0]) if tb else 0))
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "4"))):
         for pt in pts:
             for name, (L, h) in libs.items():
-                k, w, o, f, sp = pt
+                k, w, o, f, sp, tb = pt
                 assert L.s3dg_set_waves_per_block(h, w) == 0
                 assert L.s3dg_set_occupancy(h, o, o) == 0
                 assert L.s3dg_set_batch_prefetch(h, u32(f)) == 0
                 assert L.s3dg_set_store_policy(h, sp, sp) == 0
+                assert L.s3dg_set_batch_tile(h, u32(tb)) == 0
                 run(L, h, k)
                 torch.cuda.synchronize()
                 if k == "crc":
