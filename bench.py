@@ -82,7 +82,7 @@ def parse():
     p.add_argument("--occupancy", type=int, default=None,
                    help="resident fill workgroups per CU cap (default: library's, 14 stream / none batch)")
     p.add_argument("--prefetch", type=int, default=None,
-                   help="batch tile-record prefetch distance in tiles (default: library's, 128)")
+                   help="batch tile-record prefetch distance in 64-block units (default: library's, 256)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")

@@ -78,8 +78,9 @@ int s3dg_set_store_policy(s3dg_ctx *ctx, int stream_policy, int batch_policy);
  * batch launches separately; 0 = hardware maximum, negative = the default.
  * Defaults 14 (stream) and 0 (batch), measured on MI355X.  A tuning knob; results are identical. */
 int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_cu);
-/* Batch launches: distance (in 64-block tiles) at which workgroups warm the
- * L2 with a later tile record; 0 = off.  Default 128.  Results are identical. */
+/* Batch launches: distance (in units of 64 blocks) at which workgroups warm
+ * the L2 with later tile records; 0 = off, UINT32_MAX = default (256).
+ * Results are identical. */
 int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
 /* Batch launches: blocks per tile record (8, 16, 32 or 64); 0 = chosen per
  * launch from the object sizes (default).  Results are identical. */

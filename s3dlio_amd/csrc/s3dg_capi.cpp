@@ -30,6 +30,7 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 using namespace s3dg;
 
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
+constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident workgroups / 64
 constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
@@ -49,7 +50,7 @@ struct s3dg_ctx {
     // resident fill workgroups per CU (0 = hardware max); measured on MI355X
     // (DESIGN.md §5.1): 14 for 2-wave stream blocks, no cap for 1-wave batch blocks
     int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
-    uint32_t prefetch_tiles = 128;     // batch tile-record prefetch distance
+    uint32_t prefetch_tiles = kDefaultPrefetch;   // batch tile-record prefetch distance
     uint32_t tile_shift = 0;           // batch tile = 2^tile_shift blocks; 0 = per launch
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
@@ -153,9 +154,7 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // XCD) per tile.  Pick the tile size that minimises launched workgroups +
 // kTileCost x records.
 constexpr uint64_t kTileCost = 2;
-#ifndef S3DG_XCD_ALIGN
-#define S3DG_XCD_ALIGN 1
-#endif
+
 uint32_t pick_tile_shift(const uint64_t (&ntiles)[kTileShiftMax + 1]) {
     uint32_t best = kTileShiftMax;
     uint64_t best_cost = UINT64_MAX;
@@ -293,7 +292,7 @@ int s3dg_set_occupancy(s3dg_ctx *c, int stream_wgs_per_cu, int batch_wgs_per_cu)
 
 int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
     if (!c) return fail(S3DG_EINVAL, "null context");
-    c->prefetch_tiles = tiles;
+    c->prefetch_tiles = tiles == UINT32_MAX ? kDefaultPrefetch : tiles;
     return S3DG_OK;
 }
 
@@ -468,7 +467,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         e.size = d[k].size;
         e.entropy = d[k].entropy;
         // XCD alignment: slot (mod 8) = 4 KiB granule (mod 8) of the block's address
-        e.lead = S3DG_XCD_ALIGN ? (uint32_t)((((uintptr_t)dst_base + d[k].dst_off) >> 12) & 7) : 0;
+        e.lead = (uint32_t)((((uintptr_t)dst_base + d[k].dst_off) >> 12) & 7);
         e.pad = 0;
         e.tile_begin = nb + e.lead;   // slot count until the tile size is known
         if (int r = make_prefix(nb, d[k].dedup, d[k].f_num, d[k].f_den, &e.pp)) return r;

@@ -330,12 +330,11 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
     gen_block<NT, NW, true>(dst_base + e.dst_off + (uint64_t)ib * kBlk, S, t, wave, (uint32_t)ib, e.size,
                             e.entropy, e.pp, B);
-#ifndef S3DG_PF_SPAN
-#define S3DG_PF_SPAN 256
-#endif
-    // one prefetching workgroup per XCD per span blocks; lane q of it
-    // touches the q-th 128-byte line (2 records) of the span's records
-    const uint32_t span = (uint32_t)S3DG_PF_SPAN > (2u << tshift) ? (uint32_t)S3DG_PF_SPAN : (2u << tshift);
+    // one prefetching workgroup per XCD per span blocks (256: 128 and 512
+    // measured slower); lane q of it touches the q-th
+    // 128-byte line (2 records) of the span's records
+    constexpr uint32_t kPfSpan = 256;
+    const uint32_t span = kPfSpan > (2u << tshift) ? kPfSpan : (2u << tshift);
     if (pf && (g & (span - 1)) < 8 && t < (span >> (tshift + 1))) {
         const uint64_t pt = (((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift) + 2 * t;
         const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
@@ -388,9 +387,33 @@ __global__ __launch_bounds__(64 * NW) void k_write_ceiling(uint8_t *dst, uint64_
 // 64/P rows per store instruction, so every store covers whole 8D-byte row
 // segments (D = 16: 128 B, 8 rows per instruction; D = 64: 512 B, 2 rows).
 // W waves per workgroup; LDS = W * 64 * (8D + 16) bytes.
+// a ^ b ^ c on 64-bit lanes: two v_bitop3_b32 (gfx950 3-input LUT op, 0x96 =
+// XOR3) instead of four v_xor_b32; the compiler does not form it itself.
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32),
+                                                    (uint32_t)(c >> 32), 0x96);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// a ^ (s & m) with a 32-bit mask m applied to both halves: v_bitop3 0x6C =
+// S1 ^ (S0 & S2) (symmetric in S0, S2, so independent of the LUT's bit order).
+__device__ __forceinline__ uint64_t and_xor_64(uint64_t s, uint64_t a, uint32_t m) {
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)s, (uint32_t)a, m, 0x6C);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(s >> 32), (uint32_t)(a >> 32), m, 0x6C);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// One Xoshiro256 state step (per lane, VALU): the reference order
+// s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45)
+// with the chained XORs folded into 3-input ones (11 VALU ops, was 13).
 __device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2, uint64_t &s3) {
     const uint64_t t = s1 << 17;
-    s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotlk<45>(s3);
+    const uint64_t n1 = xor3_64(s1, s2, s0);
+    const uint64_t n0 = xor3_64(s0, s3, s1);
+    const uint64_t n2 = xor3_64(s2, s0, t);
+    s3 = rotlk<45>(s3 ^ s1);
+    s0 = n0; s1 = n1; s2 = n2;
 }
 
 template <int D, int W, int SP>
@@ -476,14 +499,20 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     }
 
     if (lpc > 1 && sub > 0) {                    // jump to draw sub*span
-        const uint64_t *J = jtab + 4 * sub;
-        const uint64_t j0 = J[0], j1 = J[1], j2 = J[2], j3 = J[3];
+        // state <- sum over set bits i of J of step^i(state): 256 steps, the
+        // polynomial read as 8 32-bit halves so each step's mask is one
+        // sign-extended bit field and each accumulate one v_bitop3
+        const uint32_t *J = reinterpret_cast<const uint32_t *>(jtab + 4 * sub);
         uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        for (int i = 0; i < 256; ++i) {
-            const uint64_t jw = i < 64 ? j0 : (i < 128 ? j1 : (i < 192 ? j2 : j3));
-            const uint64_t msk = 0ull - ((jw >> (i & 63)) & 1ull);
-            a0 ^= s0 & msk; a1 ^= s1 & msk; a2 ^= s2 & msk; a3 ^= s3 & msk;
-            xo_step(s0, s1, s2, s3);
+        for (int h = 0; h < 8; ++h) {
+            const uint32_t jw = J[h];
+#pragma unroll 4
+            for (int b = 0; b < 32; ++b) {
+                const uint32_t m = (uint32_t)((int32_t)(jw << (31 - b)) >> 31);
+                a0 = and_xor_64(s0, a0, m); a1 = and_xor_64(s1, a1, m);
+                a2 = and_xor_64(s2, a2, m); a3 = and_xor_64(s3, a3, m);
+                xo_step(s0, s1, s2, s3);
+            }
         }
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }

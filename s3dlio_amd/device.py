@@ -151,9 +151,10 @@ class Context:
         default); results are identical."""
         call("s3dg_set_occupancy", self._h, int(stream_wgs_per_cu), int(batch_wgs_per_cu))
 
-    def set_batch_prefetch(self, tiles: int) -> None:
-        """Tile-record prefetch distance of batch launches (0 = off); results are identical."""
-        call("s3dg_set_batch_prefetch", self._h, int(tiles))
+    def set_batch_prefetch(self, tiles: int = -1) -> None:
+        """Tile-record prefetch distance of batch launches in units of 64 blocks
+        (0 = off, negative = library default); results are identical."""
+        call("s3dg_set_batch_prefetch", self._h, 0xFFFFFFFF if int(tiles) < 0 else int(tiles))
 
     def set_batch_tile(self, blocks: int = 0) -> None:
         """Blocks per batch tile record: 8, 16, 32, 64, or 0 = chosen per launch;

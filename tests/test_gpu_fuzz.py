@@ -43,7 +43,7 @@ def _knobs(ctx, rnd):
     ctx.set_occupancy(occ, occ)
     sp = rnd.choice([-1, 0, 1, 2, 3])
     ctx.set_store_policy(sp, sp)
-    ctx.set_batch_prefetch(rnd.choice([0, 1, 7, 128, 1 << 20]))
+    ctx.set_batch_prefetch(rnd.choice([-1, 0, 1, 7, 128, 256, 1 << 20]))
     ctx.set_batch_tile(rnd.choice([0, 0, 8, 16, 32, 64]))
 
 
@@ -51,7 +51,7 @@ def _reset(ctx):
     ctx.set_waves_per_block(0)
     ctx.set_occupancy(-1, -1)
     ctx.set_store_policy(-1, -1)
-    ctx.set_batch_prefetch(128)
+    ctx.set_batch_prefetch(-1)
     ctx.set_batch_tile(0)
     ctx.set_keystream_shape(0)
     ctx.set_keystream_shape(1)

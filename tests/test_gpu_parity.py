@@ -133,7 +133,7 @@ def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, p
         assert (got[o + sz:end] == GUARD).all()
     gpu_ctx.set_waves_per_block(0)
     gpu_ctx.set_occupancy(-1, -1)
-    gpu_ctx.set_batch_prefetch(128)
+    gpu_ctx.set_batch_prefetch(-1)
     gpu_ctx.set_store_policy(-1, -1)
     gpu_ctx.set_batch_tile(0)
 

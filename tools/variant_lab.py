@@ -5,7 +5,8 @@ extra -D flags (LAB_VARIANTS="name=-DFOO=1 -DBAR=2;name2=").  Points as in
 tools/batch_lab.py: "kind:waves:occ:pf:store[:tile];..." with kind in
 stream2 (cfg2 stream), stream3 (cfg3 stream), cfg4 (log-uniform batch),
 cfg7 (uniform 8 MiB batch), small (log-uniform 4 KiB-1 MiB batch), mid
-(uniform 1 MiB + 123 B batch), ceiling (store-only kernel), crc (s3dg_crc32).
+(uniform 1 MiB + 123 B batch), ceiling (store-only kernel), crc (s3dg_crc32),
+k2 (2 MiB keystream chunks; fields waves:wgs_per_cu:min_lane_draws:store).
 
     LAB_VARIANTS=... python tools/variant_lab.py --build-only   # here
     LAB_VARIANTS=... LAB_POINTS=... python tools/variant_lab.py # GPU box
@@ -73,7 +74,7 @@ def main():
             off += (sz + 4095) // 4096 * 4096
         descs[kind] = (arr, sum(sizes), off)
     crcs = {}
-    work = {"stream2": 8 * MiB * n, "stream3": 8 * MiB * n, "stream5": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
+    work = {"stream2": 8 * MiB * n, "k2": 8 * MiB * n, "stream3": 8 * MiB * n, "stream5": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
             **{k: v[1] for k, v in descs.items()}}
     buf = torch.empty(max([8 * MiB * n] + [v[2] for v in descs.values()]), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
@@ -85,6 +86,8 @@ def main():
             d, fn, fd = {"stream2": (1, 0, 1), "stream3": (4, 1, 2), "stream5": (2, 2, 3)}[kind]
             r = L.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(d), u32(fn), u32(fd),
                                               u64(SEED_BASE), u64(0), sh)
+        elif kind == "k2":                   # xoshiro keystream, 2 MiB chunks
+            r = L.s3dg_xoshiro_fill(h, p, u64(8 * MiB * n), u64(2 * MiB), u64(0), sh)
         elif kind == "ceiling":
             r = L.s3dg_write_ceiling(h, p, u64(8 * MiB * n), u32(0xA5A5A5A5), sh)
         elif kind == "crc":                  # synchronous: device regions + host fold
@@ -108,6 +111,8 @@ def main():
                 assert L.s3dg_set_batch_prefetch(h, u32(f)) == 0
                 assert L.s3dg_set_store_policy(h, sp, sp) == 0
                 assert L.s3dg_set_batch_tile(h, u32(tb)) == 0
+                if k == "k2":                  # k2: waves, wgs/CU, min lane draws, store
+                    assert L.s3dg_set_keystream_shape(h, 0, 64, w, o, u64(f), sp) == 0
                 run(L, h, k)
                 torch.cuda.synchronize()
                 if k == "crc":
