@@ -77,6 +77,8 @@ def parse():
     p.add_argument("--ring-gib", type=float, default=80.0,
                    help="device output ring per GPU (objects wrap when the step exceeds it)")
     p.add_argument("--waves-per-block", type=int, default=None, help="1, 2 or 4 (default 2)")
+    p.add_argument("--stream-tiles", type=int, default=-1,
+                   help="1: uniform streams through the tiled batch kernel, 0: 2D stream kernel, -1: library default")
     p.add_argument("--store", choices=["default", "plain", "nt", "sc1", "ntsc1"], default="default",
                    help="fill-kernel store cache policy (default: library's, nt sc1 stream / sc1 batch)")
     p.add_argument("--occupancy", type=int, default=None,
@@ -127,6 +129,7 @@ def main() -> int:
     ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block)
     store = {"default": -1, "plain": 0, "nt": 1, "sc1": 2, "ntsc1": 3}[args.store]
     ctx.set_store_policy(store, store)
+    ctx.set_stream_tiles(args.stream_tiles)
     if args.occupancy is not None:
         ctx.set_occupancy(args.occupancy, args.occupancy)
     if args.prefetch is not None:
@@ -186,7 +189,11 @@ def main() -> int:
             launches.append(("batch", arr, b1 - b0))
         step_bytes = sum(sizes)
     base_ptr = int(ring.data_ptr())
-    batch = cfg["size"] is None
+    # large uniform streams run through the tiled batch kernel unless --stream-tiles 0
+    # (s3dg_set_stream_tiles; 8 MiB objects are 32 KiB-aligned to each other)
+    tiled = (cfg["size"] is not None and not cfg.get("keystream") and args.stream_tiles != 0
+             and all(L[0] == "stream" and L[3] * ((L[1] + 4095) // 4096) >= 16384 for L in launches))
+    batch = cfg["size"] is None or tiled
     if cfg.get("keystream"):
         launch_shape = ("k_keystream<64,4>: 128 lanes x 2048 draws per 2 MiB chunk (jump-ahead), "
                         "64-draw LDS stage per lane, 512-B row pieces per store")
@@ -271,12 +278,13 @@ def main() -> int:
     # for pure stores on MI355X (tools/batch_lab.py); the largest is the ceiling
     ceil_bytes = min(int(ring.numel()), 16 * GiB) // 4096 * 4096
 
-    def ceiling_rate():
-        ctx.write_ceiling(ring, ceil_bytes, stream=stream)
+    def ceiling_rate(fn=None):
+        fn = fn or ctx.write_ceiling
+        fn(ring, ceil_bytes, stream=stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(3):
-            ctx.write_ceiling(ring, ceil_bytes, stream=stream)
+            fn(ring, ceil_bytes, stream=stream)
         e1.record(stream)
         torch.cuda.synchronize()
         return 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
@@ -288,7 +296,12 @@ def main() -> int:
         ctx.set_occupancy(occ, occ)
         ctx.set_store_policy(sp, sp)
         ceil_shapes[f"{waves}w_{ctx.query_occupancy()}perCU_{names[sp]}"] = round(ceiling_rate(), 1)
+    # the tiled fill's shape: batch knobs (1 wave, uncapped, sc1) + trailing record loads
+    ctx.set_waves_per_block(args.waves_per_block or 0)
+    ctx.set_occupancy(-1 if args.occupancy is None else args.occupancy, -1 if args.occupancy is None else args.occupancy)
     ctx.set_store_policy(store, store)
+    ceil_shapes[f"tiled_1w_{ctx.query_occupancy(batch=True)}perCU_{names[store]}"] = round(
+        ceiling_rate(ctx.write_ceiling_tiled), 1)
     ceiling_gbs = max(ceil_shapes.values())
     ctx.set_waves_per_block(args.waves_per_block or 0)
     occ = -1 if args.occupancy is None else args.occupancy
@@ -328,11 +341,12 @@ def main() -> int:
                        "dedup": cfg["dedup"], "compress": list(cfg["compress"]) if isinstance(cfg["compress"], tuple) else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
                        "stores": (args.store if args.store != "default"
-                                  else ("sc1" if cfg["size"] is None else "nt sc1"))},
+                                  else ("sc1" if batch else "nt sc1"))},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic_from_profiles(args.config, int(sum(launch_bytes) / len(launch_bytes))),
-                         "kernel": "k_keystream" if cfg.get("keystream") else ("k_fill_stream" if cfg["size"] else "k_fill_batch"),
+                         "kernel": "k_keystream" if cfg.get("keystream") else (
+                             "k_fill_batch" + (" (uniform tile records)" if tiled else "") if batch else "k_fill_stream"),
                          "launch_shape": launch_shape,
                          "avg_launch_ms": round(avg_ms, 3),
                          "algorithmic_bytes_per_launch": int(sum(launch_bytes) / len(launch_bytes)),

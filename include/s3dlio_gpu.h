@@ -85,6 +85,11 @@ int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
 /* Batch launches: blocks per tile record (8, 16, 32 or 64); 0 = chosen per
  * launch from the object sizes (default).  Results are identical. */
 int s3dg_set_batch_tile(s3dg_ctx *ctx, uint32_t blocks);
+/* 1 = run large uniform streams (>= 64 MiB, objects 32 KiB-aligned relative
+ * to each other) through the tiled batch kernel with device-built tile
+ * records and the batch launch knobs; 0 = always the 2D stream kernel;
+ * negative = default (1).  Results are identical. */
+int s3dg_set_stream_tiles(s3dg_ctx *ctx, int on);
 /* Keystream kernel launch shape for mode 0 (npz keystream, s3dg_xoshiro_fill)
  * or mode 1 (DG1, s3dg_dgen_fill and the generators): draws staged per lane
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident
@@ -151,6 +156,10 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n);
  * path (roofline denominator measured on the device). */
 int s3dg_write_ceiling(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern,
                        void *stream);
+/* The same in the tiled fill shape (batch launch knobs, trailing loads of
+ * the context's tile-map records, as k_fill_batch): the ceiling for tiled
+ * batches and streams. */
+int s3dg_write_ceiling_tiled(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern, void *stream);
 
 /* ---- memory / copy helpers ------------------------------------------------ */
 int s3dg_device_alloc(s3dg_ctx *ctx, uint64_t bytes, void **out);

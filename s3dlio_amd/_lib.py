@@ -58,6 +58,7 @@ SIGNATURES = {
     "s3dg_set_occupancy": (c_int, [c_vp, c_int, c_int]),
     "s3dg_set_batch_prefetch": (c_int, [c_vp, c_u32]),
     "s3dg_set_batch_tile": (c_int, [c_vp, c_u32]),
+    "s3dg_set_stream_tiles": (c_int, [c_vp, c_int]),
     "s3dg_query_occupancy": (c_int, [c_vp, c_int, ctypes.POINTER(c_int)]),
     "s3dg_set_keystream_shape": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_u64, c_int]),
     "s3dg_query_keystream_occupancy": (c_int, [c_vp, c_int, ctypes.POINTER(c_int)]),
@@ -72,6 +73,7 @@ SIGNATURES = {
                                             c_u64, c_u64, c_vp]),
     "s3dg_fill_controlled_batch": (c_int, [c_vp, c_vp, ctypes.POINTER(ObjDesc), c_u64, c_vp]),
     "s3dg_write_ceiling": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
+    "s3dg_write_ceiling_tiled": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
     "s3dg_xoshiro_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_vp]),
     "s3dg_xoshiro_jump": (c_int, [ctypes.POINTER(c_u64), c_u64]),
     "s3dg_dgen_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),

@@ -31,6 +31,8 @@ using namespace s3dg;
 
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
 constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident workgroups / 64
+constexpr int kDefaultStreamTiles = 1;
+constexpr uint64_t kStreamTilesMinBlocks = 16384;   // smaller streams: 2D kernel, no tile-map launch
 constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
@@ -64,6 +66,8 @@ struct s3dg_ctx {
     TileRec *tile_obj = nullptr;       // per-tile records (device)
     uint64_t tile_cap = 0;
     hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
+    hipEvent_t tile_free = nullptr;    // tile map may be rewritten once this fires
+    int stream_tiles = kDefaultStreamTiles;   // uniform streams through the tiled batch kernel
     std::map<uint64_t, uint64_t *> jtabs;   // (lpc << 32 | span) -> device jump table
     void *crc_tab = nullptr;           // slicing-by-8 tables (device)
     uint32_t *crc_seg = nullptr;       // per-segment CRCs (device)
@@ -213,6 +217,8 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
     if (e != hipSuccess) { delete c; return hipfail(e, "hipMalloc(base block)"); }
     e = hipEventCreateWithFlags(&c->tab_free, hipEventDisableTiming);
     if (e != hipSuccess) { (void)hipFree(c->base_dev); delete c; return hipfail(e, "hipEventCreate"); }
+    e = hipEventCreateWithFlags(&c->tile_free, hipEventDisableTiming);
+    if (e != hipSuccess) { s3dg_ctx_destroy(c); return hipfail(e, "hipEventCreate"); }
     base_from_seed(kDefaultBaseSeed, c->base_host);
     e = hipMemcpy(c->base_dev, c->base_host, kBlk, hipMemcpyHostToDevice);
     if (e != hipSuccess) { s3dg_ctx_destroy(c); return hipfail(e, "hipMemcpy(base block)"); }
@@ -232,6 +238,7 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     if (c->crc_tab) (void)hipFree(c->crc_tab);
     if (c->crc_seg) (void)hipFree(c->crc_seg);
     if (c->tab_free) (void)hipEventDestroy(c->tab_free);
+    if (c->tile_free) (void)hipEventDestroy(c->tile_free);
     delete c;
     return S3DG_OK;
 }
@@ -418,6 +425,24 @@ int s3dg_fill_controlled(s3dg_ctx *c, void *dst, uint64_t len, uint64_t dedup, u
     return s3dg_fill_controlled_range(c, dst, len, 0, ~0ull, dedup, f_num, f_den, entropy, stream);
 }
 
+// The tile map (c->tile_obj) is shared by the context's batch and tiled
+// stream launches, which may be on different streams: grow it only once the
+// last launch reading it is done, and order the next k_tile_map after that
+// launch on the device (tile_free is recorded after every reader).  Caller
+// holds c->mu until it has recorded tile_free.
+static int tile_map_acquire(s3dg_ctx *c, uint64_t tiles, hipStream_t s) {
+    if (tiles > c->tile_cap) {
+        HIP_TRY(hipEventSynchronize(c->tile_free), "hipEventSynchronize(tile map)");
+        if (c->tile_obj) (void)hipFree(c->tile_obj);
+        c->tile_obj = nullptr; c->tile_cap = 0;
+        const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
+        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");
+        c->tile_cap = cap;
+    }
+    HIP_TRY(hipStreamWaitEvent(s, c->tile_free, 0), "hipStreamWaitEvent(tile map)");
+    return S3DG_OK;
+}
+
 int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride,
                                 uint64_t n_objs, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                                 uint64_t seed_base, uint64_t first_obj, void *stream) {
@@ -429,10 +454,36 @@ int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint6
     const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
     PrefixParams pp;
     if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
+    // Large streams whose objects all start on the same 4 KiB granule
+    // (mod 8) run through the tiled batch kernel
+    const uint32_t lead = (uint32_t)(((uintptr_t)dst >> 12) & 7);
+    if (c->stream_tiles && (n_objs == 1 || stride % (8 * kBlk) == 0) && n_objs * nb >= kStreamTilesMinBlocks &&
+        nb + lead < (1ull << 31)) {
+        uint64_t ntiles[kTileShiftMax + 1] = {};
+        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
+            ntiles[sh] = n_objs * ((nb + lead + (1ull << sh) - 1) >> sh);
+        const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
+        const uint64_t tpo = (nb + lead + (1ull << tshift) - 1) >> tshift;
+        hipStream_t s = (hipStream_t)stream;
+        std::lock_guard<std::mutex> g(c->mu);
+        if (int r = tile_map_acquire(c, n_objs * tpo, s)) return r;
+        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true), (uint8_t *)dst, obj_size, stride, n_objs,
+                                          (uint32_t)tpo, tshift, lead, seed_base + (first_obj << 32), pp,
+                                          c->tile_obj, c->base_dev, s),
+                "launch k_fill_batch(stream)");
+        HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
+        return S3DG_OK;
+    }
     HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, obj_size, stride, n_objs, 0,
                                (uint32_t)nb, seed_base, first_obj, pp, c->base_dev,
                                (hipStream_t)stream),
             "launch k_fill_stream");
+    return S3DG_OK;
+}
+
+int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    c->stream_tiles = on < 0 ? kDefaultStreamTiles : (on != 0);
     return S3DG_OK;
 }
 
@@ -482,23 +533,15 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         c->tab_host[k].tile_begin = tiles;
         tiles += (slots + (1ull << tshift) - 1) >> tshift;
     }
-    if (tiles > c->tile_cap) {
-        // the previous batch may still read the old map: it is stream-ordered
-        // only on its own stream, so drain the device before freeing
-        HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
-        if (c->tile_obj) (void)hipFree(c->tile_obj);
-        c->tile_obj = nullptr; c->tile_cap = 0;
-        const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
-        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");
-        c->tile_cap = cap;
-    }
     hipStream_t s = (hipStream_t)stream;
+    if (int r = tile_map_acquire(c, tiles, s)) return r;
     HIP_TRY(hipMemcpyAsync(c->tab_dev, c->tab_host, m * sizeof(ObjEntry), hipMemcpyHostToDevice, s),
             "hipMemcpyAsync(batch table)");
     HIP_TRY(hipEventRecord(c->tab_free, s), "hipEventRecord");
     HIP_TRY(launch_fill_batch(cfg_for(c, true), (uint8_t *)dst_base, c->tab_dev, m, tiles, tshift,
                               c->tile_obj, c->base_dev, s),
             "launch k_fill_batch");
+    HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
     return S3DG_OK;
 }
 
@@ -644,8 +687,23 @@ int s3dg_write_ceiling(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, v
     CTX_SCOPE(c);
     if (!dst || !aligned16(dst) || (len % kBlk))
         return fail(S3DG_EINVAL, "dst must be 16-byte aligned and len a multiple of 4096");
-    HIP_TRY(launch_write_ceiling(cfg_for(c), (uint8_t *)dst, len, pattern, (hipStream_t)stream),
+    HIP_TRY(launch_write_ceiling(cfg_for(c), (uint8_t *)dst, len, pattern, nullptr, 0, (hipStream_t)stream),
             "launch k_write_ceiling");
+    return S3DG_OK;
+}
+
+int s3dg_write_ceiling_tiled(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pattern, void *stream) {
+    CTX_SCOPE(c);
+    if (!dst || !aligned16(dst) || (len % kBlk))
+        return fail(S3DG_EINVAL, "dst must be 16-byte aligned and len a multiple of 4096");
+    if (len == 0) return S3DG_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t nthr = (len / kBlk + 63) / 64;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (int r = tile_map_acquire(c, nthr, s)) return r;
+    HIP_TRY(launch_write_ceiling(cfg_for(c, true), (uint8_t *)dst, len, pattern, c->tile_obj, nthr, s),
+            "launch k_write_ceiling(tiled)");
+    HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
     return S3DG_OK;
 }
 

@@ -81,6 +81,13 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
                              uint64_t n, uint64_t total_tiles, uint32_t tshift, TileRec *tiles,
                              const void *base_dev, hipStream_t s);
 
+// A uniform stream through the batch kernel: records built on the device
+// (k_tile_map_uniform), then k_fill_batch.
+hipError_t launch_fill_uniform_tiles(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size, uint64_t stride,
+                                     uint64_t n_objs, uint32_t tiles_per_obj, uint32_t tshift, uint32_t lead,
+                                     uint64_t ent0, PrefixParams pp, TileRec *tiles, const void *base_dev,
+                                     hipStream_t s);
+
 // K2 keystream launch: chunks [chunk0, chunk0 + nchunks) of an obj_len-byte
 // object, chunk k at dst + (k - chunk0) * chunk_bytes.
 struct KeystreamArgs {
@@ -111,8 +118,9 @@ hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t
                            const KsShape &sh, hipStream_t s);
 hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu);
 
+// thr/nthr: records for the tiled shape's trailing loads (lc.prefetch_tiles), or null
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
-                                uint32_t pattern, hipStream_t s);
+                                uint32_t pattern, const TileRec *thr, uint64_t nthr, hipStream_t s);
 
 
 // ---- CRC-32 (s3dg_crc.hip) -------------------------------------------------

@@ -272,24 +272,25 @@ __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, 
     for (int k = 0; k < SPL; ++k) write_block<NT>(bd, S, (int)(t + k * T) * 16);
 }
 
-// Stream: blockIdx.x = block (blk_lo + x) of object (y0 + blockIdx.y).
+// Stream: blockIdx.x = block (blk_lo + x) of object blockIdx.y of this launch
+// (dst and ent0 already advanced to the launch's first object).  Argument
+// order matters: the first 14 dwords arrive preloaded in SGPRs, the rest by
+// a scalar load from the kernarg segment, so base (needed first) and
+// everything up to the plan's first use lead and the prefix parameters trail.
 template <int NT, int NW>
-__global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, uint64_t obj_size,
-                                                     uint64_t stride, uint32_t blk_lo,
-                                                     uint64_t y0, uint64_t seed_base,
-                                                     uint64_t first_obj, PrefixParams pp,
-                                                     const u32x4 *base) {
+__global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32x4 *base, uint64_t stride,
+                                                         uint64_t ent0, uint64_t obj_size, uint32_t blk_lo,
+                                                         PrefixParams pp) {
     __shared__ __attribute__((aligned(16))) BlockLds S;
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint64_t j = y0 + blockIdx.y;
-    uint64_t jv = j;                 // block address on the VALU: keep the scalar unit
+    uint64_t jv = blockIdx.y;        // block address on the VALU: keep the scalar unit
     asm volatile("" : "+v"(jv));     // for the PRNG chain
     uint8_t *bd = dst + jv * stride + (uint64_t)blockIdx.x * kBlk;
     u32x4 B[4 / NW];
     load_base<NW>(B, t, base);
     gen_block<NT, NW>(bd, S, t, wave, blk_lo + blockIdx.x, obj_size,
-                      seed_base + ((first_obj + j) << 32), pp, B);
+                      ent0 + ((uint64_t)blockIdx.y << 32), pp, B);
 }
 
 // Batch: workgroup g -> tile record g >> tshift (one scalar load), block
@@ -318,7 +319,11 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     // overlap instead of following each other (the compiler otherwise splits
     // the record into four loads around the early-exit branch).
     u32x16 raw;
+#if S3DG_BATCH_HOTREC   // diagnostic (cfg7 layout only, wrong bytes): L2-hot records
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + (tile & 1023)) : "memory");
+#else
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + tile) : "memory");
+#endif
     u32x4 B[4 / NW];
     load_base<NW>(B, t, base);
     store_image<NW>(S, t, B);
@@ -326,10 +331,15 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(raw) :: "memory");
     const TileRec e = __builtin_bit_cast(TileRec, raw);
     const uint32_t k = (uint32_t)(g & ((1u << tshift) - 1));
+#if S3DG_BATCH_HOTREC
+    const int64_t ib = (int64_t)((tile & 31) << 6) + k;
+    uint8_t *const bdst = dst_base + (tile << 18) + (uint64_t)k * kBlk;
+#else
     const int64_t ib = (int64_t)e.first + k - e.lead;
+    uint8_t *const bdst = dst_base + e.dst_off + (uint64_t)ib * kBlk;
+#endif
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
-    gen_block<NT, NW, true>(dst_base + e.dst_off + (uint64_t)ib * kBlk, S, t, wave, (uint32_t)ib, e.size,
-                            e.entropy, e.pp, B);
+    gen_block<NT, NW, true>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
     // 128-byte line (2 records) of the span's records
@@ -363,16 +373,44 @@ __global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t 
     }
 }
 
+// tiles[q] for a uniform stream: n objects of obj_size bytes at dst_off =
+// j * stride, entropy ent0 + (j << 32), all with the same lead (stride a
+// multiple of 32 KiB), tiles_per_obj tiles each.
+__global__ __launch_bounds__(256) void k_tile_map_uniform(TileRec *tiles, uint64_t ntiles, uint32_t tiles_per_obj,
+                                                          uint32_t tshift, uint64_t stride, uint64_t obj_size,
+                                                          uint64_t ent0, uint32_t lead, PrefixParams pp) {
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= ntiles) return;
+    const uint64_t j = q / tiles_per_obj;
+    TileRec r;
+    r.dst_off = j * stride;
+    r.size = obj_size;
+    r.entropy = ent0 + (j << 32);
+    r.first = (uint32_t)((q - j * tiles_per_obj) << tshift);
+    r.lead = lead;
+    r.pp = pp;
+    tiles[q] = r;
+}
+
 // Write-only ceiling in the fill kernels' shape: one 4 KiB chunk per
-// (64*NW)-thread workgroup, 16-byte stores, same occupancy cap.
+// (64*NW)-thread workgroup, 16-byte stores, same occupancy cap.  pf > 0:
+// the tiled fill's trailing loads too (64-block records in thr, 256-block
+// spans, k_fill_batch), so the ceiling covers that shape.
 template <int NT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_write_ceiling(uint8_t *dst, uint64_t nchunks, uint64_t g0,
-                                                           uint32_t pat) {
+                                                           uint32_t pat, const TileRec *thr, uint64_t nthr,
+                                                           uint32_t pf) {
     const u32x4 v = {pat, pat ^ 0x9E3779B9u, pat + 1u, ~pat};
     const uint64_t g = g0 + blockIdx.x;
     if (g >= nchunks) return;
 #pragma unroll
     for (int k = 0; k < 4 / NW; ++k) store16<NT>(dst + g * kBlk + (threadIdx.x + k * 64 * NW) * 16, v);
+    if (pf && (g & 255) < 8 && threadIdx.x < 2) {
+        const uint64_t pt = (((g + 64ull * pf) & ~255ull) >> 6) + 2 * threadIdx.x;
+        const TileRec *p = thr + (pt < nthr ? pt : nthr - 1);
+        uint32_t dummy;
+        asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
+    }
 }
 
 
@@ -622,11 +660,9 @@ constexpr uint32_t ks_static_lds(int D, int W) { return (uint32_t)W * 64u * (uin
 constexpr uint64_t kMaxGridX = 1ull << 22;
 
 template <int NT, int NW>
-void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t obj_size, uint64_t stride,
-                       uint32_t blk_lo, uint64_t y0, uint64_t seed_base, uint64_t first_obj,
-                       PrefixParams pp, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_stream<NT, NW>), g, dim3(64 * NW), lds, s, d, obj_size, stride, blk_lo,
-                       y0, seed_base, first_obj, pp, b);
+void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const u32x4 *b, uint64_t stride,
+                       uint64_t ent0, uint64_t obj_size, uint32_t blk_lo, PrefixParams pp) {
+    hipLaunchKernelGGL((k_fill_stream<NT, NW>), g, dim3(64 * NW), lds, s, d, b, stride, ent0, obj_size, blk_lo, pp);
 }
 
 template <int NT, int NW>
@@ -637,8 +673,8 @@ void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const Til
 
 template <int NT, int NW>
 void launch_ceiling_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t nch, uint64_t g0,
-                        uint32_t pattern) {
-    hipLaunchKernelGGL((k_write_ceiling<NT, NW>), g, dim3(64 * NW), lds, s, d, nch, g0, pattern);
+                        uint32_t pattern, const TileRec *thr, uint64_t nthr, uint32_t pf) {
+    hipLaunchKernelGGL((k_write_ceiling<NT, NW>), g, dim3(64 * NW), lds, s, d, nch, g0, pattern, thr, nthr, pf);
 }
 
 #define S3DG_DISPATCH_W(SP, fn, lc, ...)                                        \
@@ -706,11 +742,26 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
         const uint32_t ny = (uint32_t)((n_objs - y0) < 65535 ? (n_objs - y0) : 65535);
         for (uint64_t x0 = 0; x0 < nx; x0 += kMaxGridX) {
             const uint32_t gx = (uint32_t)((nx - x0) < kMaxGridX ? (nx - x0) : kMaxGridX);
-            S3DG_DISPATCH(launch_stream_one, lc, dim3(gx, ny), lc.dyn_lds, s, dst + x0 * kBlk, obj_size, stride,
-                          (uint32_t)(blk_lo + x0), y0, seed_base, first_obj, pp, b);
+            S3DG_DISPATCH(launch_stream_one, lc, dim3(gx, ny), lc.dyn_lds, s, dst + y0 * stride + x0 * kBlk, b,
+                          stride, seed_base + ((first_obj + y0) << 32), obj_size, (uint32_t)(blk_lo + x0), pp);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
+    }
+    return hipSuccess;
+}
+
+static hipError_t launch_batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t total_tiles,
+                                     uint32_t tshift, TileRec *tiles, const void *base_dev, hipStream_t s) {
+    hipError_t e;
+    const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
+    const uint64_t total = total_tiles << tshift;
+    for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
+        const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
+        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
+                      lc.prefetch_tiles, tshift, b);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
@@ -722,16 +773,20 @@ hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEn
     hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tiles, tshift);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
-    const uint64_t total = total_tiles << tshift;
-    for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
-        const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
-        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
-                      lc.prefetch_tiles, tshift, b);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    return launch_batch_tiles(lc, dst_base, total_tiles, tshift, tiles, base_dev, s);
+}
+
+hipError_t launch_fill_uniform_tiles(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size, uint64_t stride,
+                                     uint64_t n_objs, uint32_t tiles_per_obj, uint32_t tshift, uint32_t lead,
+                                     uint64_t ent0, PrefixParams pp, TileRec *tiles, const void *base_dev,
+                                     hipStream_t s) {
+    (void)hipGetLastError();
+    const uint64_t total_tiles = n_objs * tiles_per_obj;
+    hipLaunchKernelGGL(k_tile_map_uniform, dim3((uint32_t)((total_tiles + 255) / 256)), dim3(256), 0, s, tiles,
+                       total_tiles, tiles_per_obj, tshift, stride, obj_size, ent0, lead, pp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_batch_tiles(lc, dst, total_tiles, tshift, tiles, base_dev, s);
 }
 
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
@@ -751,12 +806,13 @@ hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu) {
 }
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len, uint32_t pattern,
-                                hipStream_t s) {
+                                const TileRec *thr, uint64_t nthr, hipStream_t s) {
     (void)hipGetLastError();
     const uint64_t nch = len / kBlk;
+    const uint32_t pf = thr && nthr ? lc.prefetch_tiles : 0;
     for (uint64_t g0 = 0; g0 < nch; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((nch - g0) < kMaxGridX ? (nch - g0) : kMaxGridX);
-        S3DG_DISPATCH(launch_ceiling_one, lc, dim3(gx), lc.dyn_lds, s, dst, nch, g0, pattern);
+        S3DG_DISPATCH(launch_ceiling_one, lc, dim3(gx), lc.dyn_lds, s, dst, nch, g0, pattern, thr, nthr, pf);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

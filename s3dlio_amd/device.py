@@ -156,6 +156,11 @@ class Context:
         (0 = off, negative = library default); results are identical."""
         call("s3dg_set_batch_prefetch", self._h, 0xFFFFFFFF if int(tiles) < 0 else int(tiles))
 
+    def set_stream_tiles(self, on: int = -1) -> None:
+        """1: large uniform streams run through the tiled batch kernel; 0: the 2D
+        stream kernel; negative: library default.  Results are identical."""
+        call("s3dg_set_stream_tiles", self._h, int(on))
+
     def set_batch_tile(self, blocks: int = 0) -> None:
         """Blocks per batch tile record: 8, 16, 32, 64, or 0 = chosen per launch;
         results are identical."""
@@ -241,6 +246,12 @@ class Context:
                       stream=None) -> None:
         n = _nbytes(dst) if nbytes is None else nbytes
         call("s3dg_write_ceiling", self._h, _ptr(dst), int(n), int(pattern), _stream(stream))
+
+    def write_ceiling_tiled(self, dst, nbytes: int | None = None, pattern: int = 0xA5A5A5A5,
+                            stream=None) -> None:
+        """Store-only kernel in the tiled fill shape (batch knobs + trailing record loads)."""
+        n = _nbytes(dst) if nbytes is None else nbytes
+        call("s3dg_write_ceiling_tiled", self._h, _ptr(dst), int(n), int(pattern), _stream(stream))
 
     def sync(self, stream=None) -> None:
         call("s3dg_sync", self._h, 0 if stream is None else _stream(stream))

@@ -103,6 +103,45 @@ def test_stream_vs_oracle(gpu_ctx, torch, oracle, base, size, stride, n, d, c, f
     assert (got[stride * n:] == GUARD).all()
 
 
+@pytest.mark.parametrize("size,stride,n,d,c,off,tile", [
+    (8 * 2**20, 8 * 2**20, 9, 1, 1, 4096 * 3, 0),            # lead 3
+    (2**20 + 123, 2**20 + 32768, 70, 3, (3, 2), 4096 * 7, 0), # ragged tail, lead 7
+    (2**20 + 123, 2**20 + 32768, 70, 3, (3, 2), 4096 * 5, 8),
+    (3 * 2**20 + 4096 * 5, 4 * 2**20, 20, 2, 3, 16, 16),     # dst 16 B past a granule
+    (80 * 2**20 + 9, 80 * 2**20 + 16, 1, 5, 7, 4096, 32),    # one large object
+    (2**16, 2**16, 1100, 1, 2, 0, 0),                       # 16-block objects: small tiles
+])
+def test_stream_tiled_vs_oracle_and_2d(gpu_ctx, torch, oracle, base, size, stride, n, d, c, off, tile):
+    """Large uniform streams run through the tiled batch kernel (device-built
+    records, XCD lead from the destination address); every byte against the
+    oracle and against the 2D stream kernel, guard bytes around every object."""
+    fn, fd = P.compress_ratio(c)
+    out = torch.full((off + stride * n + 64,), GUARD, dtype=torch.uint8, device="cuda")
+    gpu_ctx.set_batch_tile(tile)
+    try:
+        gpu_ctx.fill_stream(out[off:], obj_size=size, n_objs=n, stride=stride, dedup=d, compress=c,
+                            seed_base=SEED_BASE, first_obj=11)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        gpu_ctx.set_stream_tiles(0)
+        out2 = torch.full_like(out, GUARD)
+        gpu_ctx.fill_stream(out2[off:], obj_size=size, n_objs=n, stride=stride, dedup=d, compress=c,
+                            seed_base=SEED_BASE, first_obj=11)
+        torch.cuda.synchronize()
+        assert bool(torch.equal(out, out2)), "tiled and 2D stream kernels differ"
+    finally:
+        gpu_ctx.set_stream_tiles(-1)
+        gpu_ctx.set_batch_tile(0)
+    exp = oracle.fill_stream(size, n, d, fn, fd, SEED_BASE, 11, base, stride=stride, threads=8)
+    assert (got[:off] == GUARD).all()
+    g = got[off:]
+    for j in range(n):
+        o = j * stride
+        assert np.array_equal(g[o:o + size], exp[o:o + size]), j
+        assert (g[o + size:o + stride] == GUARD).all(), f"gap overwritten after object {j}"
+    assert (g[stride * n:] == GUARD).all()
+
+
 @pytest.mark.parametrize("waves,occ,pf,sp,tile", [
     (1, -1, 128, -1, 0), (2, -1, 128, 0, 64), (4, -1, 128, 1, 8), (1, 0, 0, 0, 16), (1, 20, 1, 1, 32),
     (2, 12, 3, 2, 8), (1, -1, 100000, -1, 64), (2, 14, 64, 3, 0), (1, -1, 128, -1, 8), (1, 26, 0, -1, 16)])
@@ -254,6 +293,14 @@ def test_write_ceiling_kernel(gpu_ctx, torch):
     torch.cuda.synchronize()
     w = t.view(torch.int32).view(-1, 4)
     assert int(w[:, 0].eq(0x01020304).all()) == 1
+
+
+def test_write_ceiling_tiled_kernel(gpu_ctx, torch):
+    t = torch.zeros(2**26, dtype=torch.uint8, device="cuda")
+    gpu_ctx.write_ceiling_tiled(t, pattern=0x0A0B0C0D)
+    torch.cuda.synchronize()
+    w = t.view(torch.int32).view(-1, 4)
+    assert int(w[:, 0].eq(0x0A0B0C0D).all()) == 1 and int(w[:, 3].eq(~0x0A0B0C0D).all()) == 1
 
 
 def test_invalid_arguments_raise(gpu_ctx, torch):

@@ -69,26 +69,31 @@ def main():
         descs[k] = (("gs", sz, stride, cnt, d, fn, fd), stride * cnt, sz * cnt)
     descs["stream2"] = (None, 8 * MiB * n, 8 * MiB * n)
     descs["stream3"] = ("s3", 8 * MiB * n, 8 * MiB * n)        # cfg3: dedup 4, compress 2
+    descs["stream5"] = ("s5", 8 * MiB * n, 8 * MiB * n)        # cfg5: dedup 2, compress 3
+    descs["stream2t"], descs["stream3t"], descs["stream5t"] = descs["stream2"], descs["stream3"], descs["stream5"]
     descs["ceiling"] = ("c", 8 * MiB * n, 8 * MiB * n)         # store-only kernel, fill shapes
-    buf = torch.empty(max(v[1] for v in descs.values()), dtype=torch.uint8, device="cuda")
+    dst_off = int(os.environ.get("LAB_DST_OFF", "0"))      # generic s/u kinds: destination offset
+    buf = torch.empty(max(v[1] for v in descs.values()) + dst_off, dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     sh = int(st.cuda_stream)
 
     def run(name):
         arr = descs[name][0]
+        name = name.rstrip("t") if name.startswith("stream") else name
         if name == "ceiling":
             call("s3dg_write_ceiling", ctx._h, buf.data_ptr(), 8 * MiB * n, 0xA5A5A5A5, sh)
             return
         if isinstance(arr, tuple):
             _, sz, stride, cnt, d, fn, fd = arr
-            call("s3dg_fill_controlled_stream", ctx._h, buf.data_ptr(), sz, stride, cnt, d, fn, fd, SEED_BASE, 0, sh)
+            call("s3dg_fill_controlled_stream", ctx._h, buf.data_ptr() + dst_off, sz, stride, cnt, d, fn, fd,
+                 SEED_BASE, 0, sh)
             return
-        if arr is None or arr == "s3":
-            d, fn, fd = (1, 0, 1) if arr is None else (4, 1, 2)
+        if arr is None or arr in ("s3", "s5"):
+            d, fn, fd = {None: (1, 0, 1), "s3": (4, 1, 2), "s5": (2, 2, 3)}[arr]
             call("s3dg_fill_controlled_stream", ctx._h, buf.data_ptr(), 8 * MiB, 8 * MiB, n, d, fn, fd,
                  SEED_BASE, 0, sh)
         else:
-            call("s3dg_fill_controlled_batch", ctx._h, buf.data_ptr(), arr, len(arr), sh)
+            call("s3dg_fill_controlled_batch", ctx._h, buf.data_ptr() + dst_off, arr, len(arr), sh)
 
     res, occ = {}, {}
     for rep in range(int(os.environ.get("LAB_REPS", "3"))):
@@ -99,6 +104,7 @@ def main():
             ctx.set_occupancy(o, o)
             ctx.set_batch_prefetch(f)
             ctx.set_batch_tile(p[5])
+            ctx.set_stream_tiles(1 if k in ("stream2t", "stream3t", "stream5t") else 0)
             occ[p] = ctx.query_occupancy(batch=not k.startswith(("stream", "ceiling")) and not k[1:2].isdigit()
                                          or k.startswith("u"))
             run(k)
