@@ -53,6 +53,7 @@ def _reset(ctx):
     ctx.set_store_policy(-1, -1)
     ctx.set_batch_prefetch(-1)
     ctx.set_batch_tile(0)
+    ctx.set_stream_tiles(-1)
     ctx.set_keystream_shape(0)
     ctx.set_keystream_shape(1)
 
@@ -102,6 +103,43 @@ def test_fuzz_controlled_stream_batch(gpu_ctx, torch, oracle, seed):
                 assert (h[o + sz:end] == GUARD).all()
     finally:
         gpu_ctx.set_base_block(orig)
+        _reset(gpu_ctx)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_tiled_streams(gpu_ctx, torch, oracle, seed):
+    """Large uniform streams (>= 16384 blocks) take the tiled batch kernel:
+    random ragged sizes, 32 KiB-multiple strides, random destination offsets
+    (so every XCD lead 0..7 occurs) and random launch knobs."""
+    rnd = random.Random(3000 + seed)
+    base = np.frombuffer(gpu_ctx.base_block, np.uint8)
+    try:
+        for _ in range(3):
+            _knobs(gpu_ctx, rnd)
+            gpu_ctx.set_stream_tiles(1)
+            sz = rnd.randint(4096, 4 << 20) + rnd.choice([0, 0, 1, 7, 15, 4095])
+            stride = ((sz + 32767) // 32768 + rnd.randint(0, 2)) * 32768
+            blocks = (sz + 4095) // 4096
+            n = max(1, (16384 + blocks - 1) // blocks + rnd.randint(0, 8))
+            while n > 1 and n * stride > (160 << 20):
+                n -= 1
+            off = 16 * rnd.randint(0, 4096)
+            d, c = rnd.choice([1, 2, 3, 5, 64]), _compress(rnd)
+            fn, fd = P.compress_ratio(c)
+            sb, first = rnd.getrandbits(64), rnd.randint(0, 1 << 20)
+            t = torch.full((off + n * stride + 32,), GUARD, dtype=torch.uint8, device="cuda")
+            gpu_ctx.fill_stream(t[off:], obj_size=sz, n_objs=n, stride=stride, dedup=d, compress=c,
+                                seed_base=sb, first_obj=first)
+            h = t.cpu().numpy()
+            assert (h[:off] == GUARD).all()
+            g = h[off:]
+            exp = oracle.fill_stream(sz, n, d, fn, fd, sb, first, base, stride=stride, threads=8)
+            for j in range(n):
+                o = j * stride
+                assert np.array_equal(g[o:o + sz], exp[o:o + sz]), (sz, stride, n, off, j, d, c)
+                assert (g[o + sz:o + stride] == GUARD).all(), (sz, j)
+            assert (g[n * stride:] == GUARD).all()
+    finally:
         _reset(gpu_ctx)
 
 
