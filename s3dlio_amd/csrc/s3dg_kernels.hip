@@ -319,11 +319,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     // overlap instead of following each other (the compiler otherwise splits
     // the record into four loads around the early-exit branch).
     u32x16 raw;
-#if S3DG_BATCH_HOTREC   // diagnostic (cfg7 layout only, wrong bytes): L2-hot records
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + (tile & 1023)) : "memory");
-#else
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + tile) : "memory");
-#endif
     u32x4 B[4 / NW];
     load_base<NW>(B, t, base);
     store_image<NW>(S, t, B);
@@ -331,13 +327,8 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(raw) :: "memory");
     const TileRec e = __builtin_bit_cast(TileRec, raw);
     const uint32_t k = (uint32_t)(g & ((1u << tshift) - 1));
-#if S3DG_BATCH_HOTREC
-    const int64_t ib = (int64_t)((tile & 31) << 6) + k;
-    uint8_t *const bdst = dst_base + (tile << 18) + (uint64_t)k * kBlk;
-#else
     const int64_t ib = (int64_t)e.first + k - e.lead;
     uint8_t *const bdst = dst_base + e.dst_off + (uint64_t)ib * kBlk;
-#endif
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
     gen_block<NT, NW, true>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
