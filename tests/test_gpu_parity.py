@@ -142,6 +142,34 @@ def test_stream_tiled_vs_oracle_and_2d(gpu_ctx, torch, oracle, base, size, strid
     assert (g[stride * n:] == GUARD).all()
 
 
+def test_tile_map_shared_across_streams(gpu_ctx, torch, oracle, base):
+    """A batch on one stream and a tiled stream on another, back to back with
+    no host sync: both read the context's tile map, so the second k_tile_map
+    must wait for the first fill (tile_free event).  Repeated with growth."""
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    rnd = random.Random(99)
+    for rep in range(3):
+        sizes = [rnd.randint(1, 3 << 20) for _ in range(40 + 40 * rep)]
+        objs, off = [], 0
+        for j, sz in enumerate(sizes):
+            objs.append((off, sz, P.object_entropy(SEED_BASE, j), 2, 3))
+            off += (sz + 4095) // 4096 * 4096
+        a = torch.full((off,), GUARD, dtype=torch.uint8, device="cuda")
+        n, size = 12 + 4 * rep, 8 << 20
+        b = torch.full((n * size,), GUARD, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.fill_batch(a, objs, stream=s1)
+        gpu_ctx.fill_stream(b, obj_size=size, n_objs=n, dedup=1, compress=1, seed_base=SEED_BASE + rep,
+                            stream=s2)
+        torch.cuda.synchronize()
+        ha, hb = a.cpu().numpy(), b.cpu().numpy()
+        fn, fd = P.compress_ratio(3)
+        for (o, sz, e, d, c) in objs:
+            assert np.array_equal(ha[o:o + sz], oracle.fill_controlled(sz, d, fn, fd, e, base)), (rep, o)
+        exp = oracle.fill_stream(size, n, 1, 0, 1, SEED_BASE + rep, 0, base, threads=8)
+        assert np.array_equal(hb, exp), rep
+
+
 @pytest.mark.parametrize("waves,occ,pf,sp,tile", [
     (1, -1, 128, -1, 0), (2, -1, 128, 0, 64), (4, -1, 128, 1, 8), (1, 0, 0, 0, 16), (1, 20, 1, 1, 32),
     (2, 12, 3, 2, 8), (1, -1, 100000, -1, 64), (2, 14, 64, 3, 0), (1, -1, 128, -1, 8), (1, 26, 0, -1, 16)])
