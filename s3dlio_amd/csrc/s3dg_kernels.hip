@@ -596,10 +596,25 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t o = it * (D * 8) + piece * 16;               // offset within the row's region
         if (full_rows) {
+            // Pieces are read from LDS a group of 8 ahead of their stores, so
+            // each read's latency hides behind the previous group's stores
+            // (the compiler otherwise pairs each read with its store and waits
+            // P times per stage): +2 % (variant_ksgroup.log).
+            constexpr int G = P < 8 ? P : 8;
+            u32x4 v[P];
 #pragma unroll
-            for (int i = 0; i < P; ++i) {
-                const uint32_t r = R * i + l / P;
-                store16<SP>(dst + raddr[i] + o, *reinterpret_cast<const u32x4 *>(myrows + r * RS + piece * 16));
+            for (int i = 0; i < G; ++i)
+                v[i] = *reinterpret_cast<const u32x4 *>(myrows + (R * i + l / P) * RS + piece * 16);
+#pragma unroll
+            for (int g = 0; g < P; g += G) {
+                if (g + G < P) {
+#pragma unroll
+                    for (int i = g + G; i < g + 2 * G; ++i)
+                        v[i] = *reinterpret_cast<const u32x4 *>(myrows + (R * i + l / P) * RS + piece * 16);
+                }
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int i = g; i < g + G; ++i) store16<SP>(dst + raddr[i] + o, v[i]);
             }
         } else {
 #pragma unroll
