@@ -7,6 +7,7 @@ base blocks and random launch knobs (waves, occupancy, store policy,
 prefetch, batch tile size, keystream shape).  Reference semantics: src/data_gen.rs:151-224
 (fill), :102-132 (random-data layout), src/data_formats/npz.rs:376-383 (K2).
 """
+import os
 import random
 
 import numpy as np
@@ -16,6 +17,7 @@ from oracle import oracle_py as P
 
 pytestmark = pytest.mark.gpu
 GUARD = 0xA7
+SOAK = max(1, int(os.environ.get("S3DG_FUZZ_SOAK", "1")))   # soak runs: seeds x SOAK
 
 
 @pytest.fixture(scope="module")
@@ -58,7 +60,7 @@ def _reset(ctx):
     ctx.set_keystream_shape(1)
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(12 * SOAK))
 def test_fuzz_controlled_stream_batch(gpu_ctx, torch, oracle, seed):
     rnd = random.Random(1000 + seed)
     orig = gpu_ctx.base_block
@@ -106,7 +108,7 @@ def test_fuzz_controlled_stream_batch(gpu_ctx, torch, oracle, seed):
         _reset(gpu_ctx)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(6 * SOAK))
 def test_fuzz_tiled_streams(gpu_ctx, torch, oracle, seed):
     """Large uniform streams (>= 16384 blocks) take the tiled batch kernel:
     random ragged sizes, 32 KiB-multiple strides, random destination offsets
@@ -143,7 +145,7 @@ def test_fuzz_tiled_streams(gpu_ctx, torch, oracle, seed):
         _reset(gpu_ctx)
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(8 * SOAK))
 def test_fuzz_random_layout_keystream_dgen(gpu_ctx, torch, oracle, seed):
     rnd = random.Random(2000 + seed)
     base = np.frombuffer(gpu_ctx.base_block, np.uint8)
