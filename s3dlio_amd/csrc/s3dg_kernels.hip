@@ -87,17 +87,10 @@ __device__ __forceinline__ void store16(uint8_t *p, u32x4 v) {
     // hipcc neither models nor pads an asm store: a 16-byte store's data
     // registers must not be overwritten for 2 wait states after it issues
     // (cdna_hip_programming.md §5.7), so the pad is inside the string.
-#if S3DG_NO_STORE_PAD   // diagnostic only (unsafe)
-    else if constexpr (SP == kStoreSC1)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
-    else if constexpr (SP == kStoreNTSC1)
-        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
-#else
     else if constexpr (SP == kStoreSC1)
         asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
     else if constexpr (SP == kStoreNTSC1)
         asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
-#endif
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
