@@ -436,6 +436,15 @@ __device__ __forceinline__ uint64_t and_xor_64(uint64_t s, uint64_t a, uint32_t 
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Xoshiro256++ output rotl(s0 + s3, 23) + s0.  The empty asm pins the
+// rotated value as one 64-bit register pair; without it the compiler turns
+// the rotate's OR of two disjoint halves into two adds plus two moves.
+__device__ __forceinline__ uint64_t xo_out(uint64_t s0, uint64_t s3) {
+    uint64_t r = rotlk<23>(s0 + s3);
+    asm("" : "+v"(r));
+    return r + s0;
+}
+
 // One Xoshiro256 state step (per lane, VALU): the reference order
 // s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45)
 // with the chained XORs folded into 3-input ones (11 VALU ops, was 13).
@@ -565,16 +574,16 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         if (__all(it >= it_plain && it != it_tail)) {
 #pragma unroll
             for (int q = 0; q < D; q += 2) {
-                const uint64_t ra = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
-                const uint64_t rbv = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
+                const uint64_t ra = xo_out(s0, s3); xo_step(s0, s1, s2, s3);
+                const uint64_t rbv = xo_out(s0, s3); xo_step(s0, s1, s2, s3);
                 *reinterpret_cast<u32x4 *>(myrows + l * RS + q * 8) =
                     u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
             }
         } else {
 #pragma unroll
             for (int q = 0; q < D; q += 2) {
-                uint64_t ra = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
-                uint64_t rbv = rotlk<23>(s0 + s3) + s0; xo_step(s0, s1, s2, s3);
+                uint64_t ra = xo_out(s0, s3); xo_step(s0, s1, s2, s3);
+                uint64_t rbv = xo_out(s0, s3); xo_step(s0, s1, s2, s3);
                 const uint64_t d = dg + q;
                 if (tail_hi && d == tail_draw) ra >>= 32;
                 if (tail_hi && d + 1 == tail_draw) rbv >>= 32;
