@@ -49,6 +49,8 @@ def main():
         return arr, off, sum(sizes)
     descs = {}
     for name, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3),
+                                   # cfg4 sizes rounded up to whole 64-block tiles: no dead slots
+                                   ("cfg4r", [(s + (1 << 18) - 1) >> 18 << 18 for s in log_uniform_sizes(n)], 2, 1, 3),
                                    ("cfg7", [8 * MiB] * n, 1, 0, 1),
                                    ("small", log_uniform_sizes(10 * n, 5, 4096, MiB), 1, 0, 1),
                                    ("mid", [MiB + 123] * (5 * n), 3, 2, 3),
