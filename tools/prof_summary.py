@@ -7,7 +7,7 @@
   profiles/<round>/timing_cfgN.json        per-step fill time from the trace
                                            (warmup dispatches excluded) next to
                                            bench.py's HIP-event avg_launch_ms
-  profiles/traffic.json                    HBM bytes per bench launch (cfg 2, 4)
+  profiles/traffic.json                    HBM bytes per bench launch (cfg 2, 4, 6)
 
 PMC units/corrections follow MI355X_MICROARCH.md (HBM/rocprofv3 section):
 WRITE_SIZE x 1024 B; FETCH_SIZE x 1024 x 2 (gfx950 half-count).
@@ -29,7 +29,8 @@ def main(src, rnd):
     os.makedirs(dst, exist_ok=True)
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
-    for c in (2, 4):
+    for c in (2, 4, 6):
+        kern = "k_keystream" if c == 6 else "k_fill_"
         tr = os.path.join(src, f"trace_cfg{c}")
         if not os.path.isdir(tr):
             continue
@@ -38,7 +39,7 @@ def main(src, rnd):
         b = bench_line(os.path.join(src, f"bench_trace_cfg{c}.log"))
         steps, warm = b["steps"], b["warmup"]
         rows = [r for r in csv.DictReader(open(os.path.join(tr, "run_kernel_trace.csv")))
-                if "k_fill_" in r["Kernel_Name"]]
+                if kern in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         per_step = len(rows) // (steps + warm)
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows]
@@ -63,7 +64,7 @@ def main(src, rnd):
             p = os.path.join(src, f"pmc_{ctr}_cfg{c}", "run_counter_collection.csv")
             if not os.path.exists(p):
                 break
-            rr = [r for r in csv.DictReader(open(p)) if "k_fill_" in r["Kernel_Name"]]
+            rr = [r for r in csv.DictReader(open(p)) if kern in r["Kernel_Name"]]
             with open(os.path.join(dst, f"pmc_{ctr.lower()}_cfg{c}.csv"), "w", newline="") as f:
                 w = csv.DictWriter(f, fieldnames=list(rr[0].keys()))
                 w.writeheader()

@@ -6,7 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
-for c in 2 4; do
+for c in 2 4 6; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_cfg$c -o run --output-format csv -- \
       python3 bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline --no-d2h > $OUT/bench_trace_cfg$c.log 2>&1 || exit 1
   for ctr in WRITE_SIZE FETCH_SIZE; do
