@@ -111,7 +111,8 @@ int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
 uint64_t s3dg_object_entropy(uint64_t seed_base, uint64_t j);
 
 /* ---- device-resident generation (asynchronous on `stream`) -------------- */
-/* One object of `len` bytes at dst (device). */
+/* One object of `len` bytes at dst (device).  From 64 MiB up this runs as a
+ * one-object stream on the tiled kernel (s3dg_set_stream_tiles). */
 int s3dg_fill_controlled(s3dg_ctx *ctx, void *dst, uint64_t len, uint64_t dedup,
                          uint32_t f_num, uint32_t f_den, uint64_t entropy,
                          void *stream);

@@ -358,6 +358,11 @@ int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t bl
     if (blk_hi > nb) blk_hi = nb;
     if (blk_lo >= blk_hi) return S3DG_OK;
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
+    // a whole large buffer is a one-object stream: the tiled kernel (entropy
+    // of stream object 0 with seed_base = entropy is entropy itself)
+    if (blk_lo == 0 && blk_hi == nb && c->stream_tiles && nb >= kStreamTilesMinBlocks)
+        return s3dg_fill_controlled_stream(c, dst, len, (len + 15) & ~15ull, 1, dedup, f_num, f_den, entropy, 0,
+                                           stream);
     PrefixParams pp;
     if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
     HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, len, 0, 1, (uint32_t)blk_lo,

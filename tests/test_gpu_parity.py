@@ -142,6 +142,29 @@ def test_stream_tiled_vs_oracle_and_2d(gpu_ctx, torch, oracle, base, size, strid
     assert (g[stride * n:] == GUARD).all()
 
 
+@pytest.mark.parametrize("L,d,c,off", [(70 * 2**20 + 13, 3, (5, 3), 4096 * 5), (64 * 2**20, 1, 1, 0),
+                                       (96 * 2**20 + 4095, 2, 4, 48)])
+def test_large_fill_controlled_tiled(gpu_ctx, torch, oracle, base, L, d, c, off):
+    """A whole buffer >= 64 MiB runs as a one-object tiled stream; against the
+    oracle and the 2D kernel, with guard bytes."""
+    fn, fd = P.compress_ratio(c)
+    e = P.object_entropy(SEED_BASE, 77)
+    t = torch.full((off + L + 32,), GUARD, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_controlled(t[off:], L, dedup=d, compress=c, entropy=e)
+    torch.cuda.synchronize()
+    h = t.cpu().numpy()
+    try:
+        gpu_ctx.set_stream_tiles(0)
+        t2 = torch.full_like(t, GUARD)
+        gpu_ctx.fill_controlled(t2[off:], L, dedup=d, compress=c, entropy=e)
+        torch.cuda.synchronize()
+        assert bool(torch.equal(t, t2)), "tiled and 2D kernels differ"
+    finally:
+        gpu_ctx.set_stream_tiles(-1)
+    assert (h[:off] == GUARD).all() and (h[off + L:] == GUARD).all()
+    assert np.array_equal(h[off:off + L], oracle.fill_controlled(L, d, fn, fd, e, base))
+
+
 def test_tile_map_shared_across_streams(gpu_ctx, torch, oracle, base):
     """A batch on one stream and a tiled stream on another, back to back with
     no host sync: both read the context's tile map, so the second k_tile_map
