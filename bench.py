@@ -18,6 +18,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
 from __future__ import annotations
 
 import argparse
+import ctypes
 import hashlib
 import json
 import math
@@ -302,6 +303,14 @@ def main() -> int:
     ctx.set_store_policy(store, store)
     ceil_shapes[f"tiled_1w_{ctx.query_occupancy(batch=True)}perCU_{names[store]}"] = round(
         ceiling_rate(ctx.write_ceiling_tiled), 1)
+    # the runtime's own fill (SURVEY.md §8d names it as a ceiling option)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemsetD32Async.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+
+    def memset_d32(buf, nbytes, stream):
+        sh = int(getattr(stream, "cuda_stream", stream or 0))
+        assert hip.hipMemsetD32Async(buf.data_ptr(), 0x5A5A5A5A, nbytes // 4, sh) == 0
+    ceil_shapes["hipMemsetD32Async"] = round(ceiling_rate(memset_d32), 1)
     ceiling_gbs = max(ceil_shapes.values())
     ctx.set_waves_per_block(args.waves_per_block or 0)
     occ = -1 if args.occupancy is None else args.occupancy
