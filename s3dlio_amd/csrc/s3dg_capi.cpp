@@ -349,6 +349,53 @@ int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
     return S3DG_OK;
 }
 
+// The tile map (c->tile_obj) is shared by the context's batch and tiled
+// stream launches, which may be on different streams: grow it only once the
+// last launch reading it is done, and order the next k_tile_map after that
+// launch on the device (tile_free is recorded after every reader).  Caller
+// holds c->mu until it has recorded tile_free.
+static int tile_map_acquire(s3dg_ctx *c, uint64_t tiles, hipStream_t s) {
+    if (tiles > c->tile_cap) {
+        HIP_TRY(hipEventSynchronize(c->tile_free), "hipEventSynchronize(tile map)");
+        if (c->tile_obj) (void)hipFree(c->tile_obj);
+        c->tile_obj = nullptr; c->tile_cap = 0;
+        const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
+        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");
+        c->tile_cap = cap;
+    }
+    HIP_TRY(hipStreamWaitEvent(s, c->tile_free, 0), "hipStreamWaitEvent(tile map)");
+    return S3DG_OK;
+}
+
+// n_objs objects of obj_size bytes at dst + j*stride, entropy seed_base +
+// ((first_obj + j) << 32), prefix parameters pp.  Large streams whose objects
+// all start on the same 4 KiB granule (mod 8) run through the tiled batch
+// kernel; the rest through the 2D stream kernel.
+static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t stride, uint64_t n_objs,
+                        const PrefixParams &pp, uint64_t seed_base, uint64_t first_obj, hipStream_t s) {
+    const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
+    const uint32_t lead = (uint32_t)(((uintptr_t)dst >> 12) & 7);
+    if (c->stream_tiles && (n_objs == 1 || stride % (8 * kBlk) == 0) && n_objs * nb >= kStreamTilesMinBlocks &&
+        nb + lead < (1ull << 31)) {
+        uint64_t ntiles[kTileShiftMax + 1] = {};
+        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
+            ntiles[sh] = n_objs * ((nb + lead + (1ull << sh) - 1) >> sh);
+        const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
+        const uint64_t tpo = (nb + lead + (1ull << tshift) - 1) >> tshift;
+        std::lock_guard<std::mutex> g(c->mu);
+        if (int r = tile_map_acquire(c, n_objs * tpo, s)) return r;
+        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
+                                          lead, seed_base + (first_obj << 32), pp, c->tile_obj, c->base_dev, s),
+                "launch k_fill_batch(stream)");
+        HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
+        return S3DG_OK;
+    }
+    HIP_TRY(launch_fill_stream(cfg_for(c), dst, obj_size, stride, n_objs, 0, (uint32_t)nb, seed_base, first_obj,
+                               pp, c->base_dev, s),
+            "launch k_fill_stream");
+    return S3DG_OK;
+}
+
 int s3dg_fill_controlled_range(s3dg_ctx *c, void *dst, uint64_t len, uint64_t blk_lo,
                                uint64_t blk_hi, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                                uint64_t entropy, void *stream) {
@@ -383,10 +430,7 @@ int s3dg_random_data(s3dg_ctx *c, void *dst, uint64_t len, uint64_t entropy, voi
     pp.f_den = 0;                       // random-data layout
     pp.m_unique = fastmod_magic(1);
     pp.m_fden = fastmod_magic(1);
-    HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, len, 0, 1, 0, (uint32_t)nb, entropy, 0,
-                               pp, c->base_dev, (hipStream_t)stream),
-            "launch k_fill_stream(random data)");
-    return S3DG_OK;
+    return fill_uniform(c, (uint8_t *)dst, len, (len + 15) & ~15ull, 1, pp, entropy, 0, (hipStream_t)stream);
 }
 
 // The context's device (callers make it current with a DeviceScope).
@@ -430,24 +474,6 @@ int s3dg_fill_controlled(s3dg_ctx *c, void *dst, uint64_t len, uint64_t dedup, u
     return s3dg_fill_controlled_range(c, dst, len, 0, ~0ull, dedup, f_num, f_den, entropy, stream);
 }
 
-// The tile map (c->tile_obj) is shared by the context's batch and tiled
-// stream launches, which may be on different streams: grow it only once the
-// last launch reading it is done, and order the next k_tile_map after that
-// launch on the device (tile_free is recorded after every reader).  Caller
-// holds c->mu until it has recorded tile_free.
-static int tile_map_acquire(s3dg_ctx *c, uint64_t tiles, hipStream_t s) {
-    if (tiles > c->tile_cap) {
-        HIP_TRY(hipEventSynchronize(c->tile_free), "hipEventSynchronize(tile map)");
-        if (c->tile_obj) (void)hipFree(c->tile_obj);
-        c->tile_obj = nullptr; c->tile_cap = 0;
-        const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
-        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");
-        c->tile_cap = cap;
-    }
-    HIP_TRY(hipStreamWaitEvent(s, c->tile_free, 0), "hipStreamWaitEvent(tile map)");
-    return S3DG_OK;
-}
-
 int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride,
                                 uint64_t n_objs, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                                 uint64_t seed_base, uint64_t first_obj, void *stream) {
@@ -459,31 +485,7 @@ int s3dg_fill_controlled_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint6
     const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
     PrefixParams pp;
     if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) return r;
-    // Large streams whose objects all start on the same 4 KiB granule
-    // (mod 8) run through the tiled batch kernel
-    const uint32_t lead = (uint32_t)(((uintptr_t)dst >> 12) & 7);
-    if (c->stream_tiles && (n_objs == 1 || stride % (8 * kBlk) == 0) && n_objs * nb >= kStreamTilesMinBlocks &&
-        nb + lead < (1ull << 31)) {
-        uint64_t ntiles[kTileShiftMax + 1] = {};
-        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
-            ntiles[sh] = n_objs * ((nb + lead + (1ull << sh) - 1) >> sh);
-        const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
-        const uint64_t tpo = (nb + lead + (1ull << tshift) - 1) >> tshift;
-        hipStream_t s = (hipStream_t)stream;
-        std::lock_guard<std::mutex> g(c->mu);
-        if (int r = tile_map_acquire(c, n_objs * tpo, s)) return r;
-        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true), (uint8_t *)dst, obj_size, stride, n_objs,
-                                          (uint32_t)tpo, tshift, lead, seed_base + (first_obj << 32), pp,
-                                          c->tile_obj, c->base_dev, s),
-                "launch k_fill_batch(stream)");
-        HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
-        return S3DG_OK;
-    }
-    HIP_TRY(launch_fill_stream(cfg_for(c), (uint8_t *)dst, obj_size, stride, n_objs, 0,
-                               (uint32_t)nb, seed_base, first_obj, pp, c->base_dev,
-                               (hipStream_t)stream),
-            "launch k_fill_stream");
-    return S3DG_OK;
+    return fill_uniform(c, (uint8_t *)dst, obj_size, stride, n_objs, pp, seed_base, first_obj, (hipStream_t)stream);
 }
 
 int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {

@@ -165,6 +165,26 @@ def test_large_fill_controlled_tiled(gpu_ctx, torch, oracle, base, L, d, c, off)
     assert np.array_equal(h[off:off + L], oracle.fill_controlled(L, d, fn, fd, e, base))
 
 
+@pytest.mark.parametrize("L,off", [(80 * 2**20 + 5, 4096 * 3), (64 * 2**20, 0)])
+def test_large_random_data_tiled(gpu_ctx, torch, oracle, base, L, off):
+    """Random-data layout (A6 analogue) at >= 64 MiB: tiled kernel vs oracle and 2D kernel."""
+    e = 0x1234567890ABCDEF
+    t = torch.full((off + L + 32,), GUARD, dtype=torch.uint8, device="cuda")
+    gpu_ctx.random_data(t[off:], L, entropy=e)
+    torch.cuda.synchronize()
+    h = t.cpu().numpy()
+    try:
+        gpu_ctx.set_stream_tiles(0)
+        t2 = torch.full_like(t, GUARD)
+        gpu_ctx.random_data(t2[off:], L, entropy=e)
+        torch.cuda.synchronize()
+        assert bool(torch.equal(t, t2)), "tiled and 2D kernels differ"
+    finally:
+        gpu_ctx.set_stream_tiles(-1)
+    assert (h[:off] == GUARD).all() and (h[off + L:] == GUARD).all()
+    assert np.array_equal(h[off:off + L], oracle.random_data(L, e, base))
+
+
 def test_tile_map_shared_across_streams(gpu_ctx, torch, oracle, base):
     """A batch on one stream and a tiled stream on another, back to back with
     no host sync: both read the context's tile map, so the second k_tile_map
