@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — device-resident synthetic-payload GiB/s (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
 
 A "step" is one pass of the hot path over one batch: every object of the
 configuration generated once into HBM by the gfx950 kernel (src/data_gen.rs
@@ -11,9 +11,18 @@ N>1: launched by torch.distributed.run, one rank per GPU; each rank owns its
 own object-index range (weak scaling, no data-path collective; a gloo
 control plane does the barrier and the max over ranks).
 
+Configs 2-5 are BASELINE.json's; the others measure the surfaces around the
+path: 6 the K2 keystream (npz.rs:376-383), 7 config 2 through
+the batch API, 8/9 config 1's 64 KiB objects on the GPU (stream / batch API),
+10 small ragged objects through the batch API, 11-13 one
+s3dg_fill_controlled call on a single 1/4/16 MiB buffer (the reference's own
+criterion shape, benches/performance_microbenchmarks.rs:43-64), 14/15 the
+DG1 byte path behind generate_data / Generator.
+
 Prints ONE JSON line on rank 0 (contract in the task statement), including
-`roofline` (kernel-event timing vs the 8 TB/s HBM peak) and `cpu_baseline`
-(the C oracle, multi-threaded, on this host — rank 0 at N=1 only).
+`roofline` (kernel-event timing vs the 8 TB/s HBM peak, and vs the fill's own
+store-only ceiling) and `cpu_baseline` (the C port of the same generator on
+this host's cores — rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -29,6 +38,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+KiB = 1 << 10
 MiB = 1 << 20
 GiB = 1 << 30
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
@@ -37,19 +47,35 @@ BASE_SEED = 0xBA5EB10C00000000
 METRIC = "device-resident synthetic-payload GiB/s, 8 MiB objects, 1/2/4/8 MI355X"
 
 CONFIGS = {
-    2: dict(name="cfg2: 10000 x 8 MiB, dedup=1 compress=1 (pure fill)", n=10000,
+    2: dict(name="cfg2: 10000 x 8 MiB, dedup=1 compress=1 (pure fill)", kind="stream", n=10000,
             size=8 * MiB, dedup=1, compress=1, scaling="weak"),
-    3: dict(name="cfg3: 10000 x 8 MiB, dedup=4 compress=2", n=10000, size=8 * MiB,
+    3: dict(name="cfg3: 10000 x 8 MiB, dedup=4 compress=2", kind="stream", n=10000, size=8 * MiB,
             dedup=4, compress=2, scaling="weak"),
-    4: dict(name="cfg4: 10000 x log-uniform 4 KiB..64 MiB, dedup=2 compress=1.5", n=10000,
+    4: dict(name="cfg4: 10000 x log-uniform 4 KiB..64 MiB, dedup=2 compress=1.5", kind="batch", n=10000,
             size=None, dedup=2, compress=(3, 2), scaling="weak"),
-    5: dict(name="cfg5: 100000 x 8 MiB, dedup=2 compress=3 (total over all GPUs)", n=100000,
+    5: dict(name="cfg5: 100000 x 8 MiB, dedup=2 compress=3 (total over all GPUs)", kind="stream", n=100000,
             size=8 * MiB, dedup=2, compress=3, scaling="strong"),
-    # not a BASELINE config: the K2 keystream (npz x-fill, npz.rs:376-383) over the cfg2 footprint
-    7: dict(name="diag: cfg2 objects (10000 x 8 MiB, d1 c1) through the batch API", n=10000,
-            size=None, dedup=1, compress=1, scaling="weak", uniform=8 * MiB),
-    6: dict(name="k2: keystream fill, 10000 x 8 MiB as 2 MiB Xoshiro256++ chunks", n=10000,
-            size=8 * MiB, dedup=1, compress=1, scaling="weak", keystream=True),
+    # not BASELINE configs: the surfaces around the path (module docstring)
+    6: dict(name="k2: keystream fill, 10000 x 8 MiB as 2 MiB Xoshiro256++ chunks", kind="keystream", n=10000,
+            size=8 * MiB, dedup=1, compress=1, scaling="weak"),
+    7: dict(name="diag: cfg2 objects (10000 x 8 MiB, d1 c1) through the batch API", kind="batch", n=10000,
+            size=None, uniform=8 * MiB, dedup=1, compress=1, scaling="weak"),
+    8: dict(name="cfg1-shape: 1000000 x 64 KiB, dedup=1 compress=1, stream API", kind="stream", n=1000000,
+            size=64 * KiB, dedup=1, compress=1, scaling="weak"),
+    9: dict(name="cfg1-shape: 1000000 x 64 KiB, dedup=1 compress=1, batch API", kind="batch", n=1000000,
+            size=None, uniform=64 * KiB, dedup=1, compress=1, scaling="weak"),
+    10: dict(name="small: 2000000 x (20 KiB + 5 B), dedup=1 compress=1, batch API", kind="batch", n=2000000,
+             size=None, uniform=20 * KiB + 5, dedup=1, compress=1, scaling="weak"),
+    11: dict(name="single buffer: 1000 x s3dg_fill_controlled on one 1 MiB buffer, d1 c1", kind="single",
+             n=1000, size=1 * MiB, dedup=1, compress=1, scaling="weak"),
+    12: dict(name="single buffer: 1000 x s3dg_fill_controlled on one 4 MiB buffer, d1 c1", kind="single",
+             n=1000, size=4 * MiB, dedup=1, compress=1, scaling="weak"),
+    13: dict(name="single buffer: 1000 x s3dg_fill_controlled on one 16 MiB buffer, d1 c1", kind="single",
+             n=1000, size=16 * MiB, dedup=1, compress=1, scaling="weak"),
+    14: dict(name="dg1: 10 x 8 GiB DG1 objects (generate_data byte path), dedup=1 compress=1", kind="dgen",
+             n=10, size=8 * GiB, dedup=1, compress=1, scaling="weak"),
+    15: dict(name="dg1: 10 x 8 GiB DG1 objects (generate_data byte path), dedup=2 compress=2", kind="dgen",
+             n=10, size=8 * GiB, dedup=2, compress=2, scaling="weak"),
 }
 
 
@@ -86,17 +112,65 @@ def parse():
                    help="resident fill workgroups per CU cap (default: library's, 14 stream / none batch)")
     p.add_argument("--prefetch", type=int, default=None,
                    help="batch tile-record prefetch distance in 64-block units (default: library's, 256)")
+    p.add_argument("--batch-tile", type=int, default=None, help="batch tile blocks (1 = dense; default: per launch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")
+    p.add_argument("--d2h-reps", type=int, default=1, help="D2H-inclusive samples (diagnosis of run-to-run spread)")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--no-ceiling", action="store_true")
     p.add_argument("--device-override", type=int, default=None,
-                   help="rehearsal only: put every rank on this device (e.g. 2 ranks on a 1-GPU box)")
+                   help="rehearsal only: put every rank on this device (e.g. 8 ranks on a 1-GPU box)")
     return p.parse_args()
 
 
 def sha(b) -> str:
     return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def source_digest() -> str:
+    """Digest of the library sources the measured kernels are built from: a
+    traffic record (profiles/traffic.json) counts only for the same digest."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "s3dlio_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".hip", ".cpp", ".h", ".c")):
+            with open(os.path.join(csrc, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    for extra in ("include/s3dlio_gpu.h", "s3dlio_amd/build.py"):
+        with open(os.path.join(ROOT, extra), "rb") as f:
+            h.update(extra.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def cpu_share() -> dict:
+    """CPUs this process may use: scheduler affinity and the cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except Exception:
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except Exception:
+            pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"threads": threads, "affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
+def cpu_model() -> str:
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        return "unknown"
 
 
 def launch_ranks(n: int) -> int:
@@ -119,7 +193,7 @@ def main() -> int:
         return launch_ranks(args.gpus)
     import torch
     from s3dlio_amd import Context, compress_ratio, object_entropy
-    from s3dlio_amd._lib import ObjDesc, lib, call
+    from s3dlio_amd._lib import ObjDesc, call
     from s3dlio_amd.shard import ControlPlane, object_range
 
     cp = ControlPlane()
@@ -127,6 +201,7 @@ def main() -> int:
     dev = cp.local_rank if args.device_override is None else args.device_override
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
+    kind = cfg["kind"]
     ctx = Context(dev, base_seed=BASE_SEED, waves_per_block=args.waves_per_block)
     store = {"default": -1, "plain": 0, "nt": 1, "sc1": 2, "ntsc1": 3}[args.store]
     ctx.set_store_policy(store, store)
@@ -135,40 +210,46 @@ def main() -> int:
         ctx.set_occupancy(args.occupancy, args.occupancy)
     if args.prefetch is not None:
         ctx.set_batch_prefetch(args.prefetch)
+    if args.batch_tile is not None:
+        ctx.set_batch_tile(args.batch_tile)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     fn, fd = compress_ratio(cfg["compress"])
+    d = cfg["dedup"]
 
     # ---- this rank's objects -------------------------------------------------------
     if cfg["scaling"] == "strong":
-        n_total = args.objects or cfg["n"]
-        lo, hi = object_range(n_total, rank, world)
+        lo, hi = object_range(args.objects or cfg["n"], rank, world)
     else:
         n_rank = args.objects or cfg["n"]
         lo, hi = rank * n_rank, (rank + 1) * n_rank
     n_rank = hi - lo
     ring_cap = int(args.ring_gib * GiB)
 
-    launches = []      # (kind, args...) executed per step, all on `sh`
-    slot_obj = {}      # ring slot -> (obj index, size, dst_off) of the last write, for verification
-    if cfg["size"] is not None:
+    launches = []      # (callable, algorithmic bytes) per launch, all on `sh`
+    samples = []       # (ring offset, check) of the step's last writes, for verification
+    sizes = None
+    if kind in ("stream", "keystream"):
         size = cfg["size"]
         stride = (size + 4095) // 4096 * 4096
         ring_objs = max(1, min(n_rank, ring_cap // stride))
         ring = torch.empty(ring_objs * stride, dtype=torch.uint8, device=f"cuda:{dev}")
-        if cfg.get("keystream"):
-            # chunk index space continues across ranks: seed_base = first chunk of the rank
-            for s0 in range(0, n_rank, ring_objs):
-                k = min(ring_objs, n_rank - s0)
-                launches.append(("keystream", k * stride, (lo + s0) * stride // (2 * MiB)))
-                slot_obj = {t: (lo + s0 + t, size, t * stride) for t in range(k)}
-        for s0 in ([] if cfg.get("keystream") else range(0, n_rank, ring_objs)):
+        base_ptr = int(ring.data_ptr())
+        for s0 in range(0, n_rank, ring_objs):
             k = min(ring_objs, n_rank - s0)
-            launches.append(("stream", size, stride, k, lo + s0))
-            for s in range(k):
-                slot_obj[s] = (lo + s0 + s, size, s * stride)
+            if kind == "keystream":
+                # chunk index space continues across ranks: seed_base = first chunk of the rank
+                c0 = (lo + s0) * stride // (2 * MiB)
+                launches.append((lambda k=k, c0=c0: call("s3dg_xoshiro_fill", ctx._h, base_ptr, k * stride,
+                                                         2 * MiB, c0, sh), k * size))
+                samples = [(t * stride, ("chunk", c0 + t * stride // (2 * MiB))) for t in range(k)]
+            else:
+                launches.append((lambda k=k, first=lo + s0: call(
+                    "s3dg_fill_controlled_stream", ctx._h, base_ptr, size, stride, k, d, fn, fd, SEED_BASE,
+                    first, sh), k * size))
+                samples = [(t * stride, ("obj", lo + s0 + t, size)) for t in range(k)]
         step_bytes = n_rank * size
-    else:
+    elif kind == "batch":
         sizes = ([cfg["uniform"]] * n_rank) if cfg.get("uniform") else log_uniform_sizes(lo + n_rank)[lo:]
         offs, cur, batch_start, batches = [], 0, 0, []
         for j, sz in enumerate(sizes):
@@ -181,41 +262,65 @@ def main() -> int:
         batches.append((batch_start, len(sizes), offs))
         ring_bytes = max(sum((s + 4095) // 4096 * 4096 for s in sizes[b0:b1]) for b0, b1, _ in batches)
         ring = torch.empty(ring_bytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        base_ptr = int(ring.data_ptr())
         for b0, b1, o in batches:
             arr = (ObjDesc * (b1 - b0))()
             for k in range(b1 - b0):
-                j = lo + b0 + k
-                arr[k] = ObjDesc(o[k], sizes[b0 + k], object_entropy(SEED_BASE, j), cfg["dedup"], fn, fd)
-                slot_obj[o[k]] = (j, sizes[b0 + k], o[k])
-            launches.append(("batch", arr, b1 - b0))
+                arr[k] = ObjDesc(o[k], sizes[b0 + k], object_entropy(SEED_BASE, lo + b0 + k), d, fn, fd)
+            launches.append((lambda arr=arr, m=b1 - b0: call("s3dg_fill_controlled_batch", ctx._h, base_ptr, arr, m,
+                                                             sh), sum(sizes[b0:b1])))
+            # the last batch overwrites the ring: only its objects are checkable
+            samples = [(o[k], ("obj", lo + b0 + k, sizes[b0 + k])) for k in range(b1 - b0)]
         step_bytes = sum(sizes)
-    base_ptr = int(ring.data_ptr())
-    # large uniform streams run through the tiled batch kernel unless --stream-tiles 0
-    # (s3dg_set_stream_tiles; 8 MiB objects are 32 KiB-aligned to each other)
-    tiled = (cfg["size"] is not None and not cfg.get("keystream") and args.stream_tiles != 0
-             and all(L[0] == "stream" and L[3] * ((L[1] + 4095) // 4096) >= 16384 for L in launches))
-    batch = cfg["size"] is None or tiled
-    if cfg.get("keystream"):
-        launch_shape = ("k_keystream<64,4>: 128 lanes x 2048 draws per 2 MiB chunk (jump-ahead), "
-                        "64-draw LDS stage per lane, 512-B row pieces per store")
+    elif kind == "single":
+        size = cfg["size"]
+        ring = torch.empty(size, dtype=torch.uint8, device=f"cuda:{dev}")
+        base_ptr = int(ring.data_ptr())
+        calls = args.objects or cfg["n"]
+
+        def single_step(size=size, calls=calls):
+            for _ in range(calls):
+                call("s3dg_fill_controlled", ctx._h, base_ptr, size, d, fn, fd, 7, sh)
+        launches.append((single_step, calls * size))
+        samples = [(0, ("single", size))]
+        step_bytes = calls * size
+    else:   # dgen
+        size = cfg["size"]
+        ring_objs = max(1, min(n_rank, ring_cap // size))
+        ring = torch.empty(ring_objs * size, dtype=torch.uint8, device=f"cuda:{dev}")
+        base_ptr = int(ring.data_ptr())
+        for j in range(n_rank):
+            t = j % ring_objs
+            launches.append((lambda t=t, j=lo + j: call("s3dg_dgen_fill", ctx._h, base_ptr + t * size, size, 0,
+                                                        1 << 40, d, fn, fd, object_entropy(SEED_BASE, j), sh),
+                             size))
+        samples = [((j % ring_objs) * size, ("dgen", lo + j)) for j in range(max(0, n_rank - ring_objs), n_rank)]
+        step_bytes = n_rank * size
+
+    # kernel and launch shape of the dominant launch
+    tiled = (kind == "stream" and args.stream_tiles != 0
+             and all(b // cfg["size"] * ((cfg["size"] + 4095) // 4096) >= 16384 for _, b in launches)
+             and cfg["size"] % (32 * KiB) == 0)
+    if kind == "keystream":
+        kernel, launch_shape = "k_keystream", ("k_keystream<64,4>: 128 lanes x 2048 draws per 2 MiB chunk "
+                                               "(jump-ahead), 64-draw LDS stage per lane, 512-B row pieces per store")
+    elif kind == "dgen":
+        kernel, launch_shape = "k_keystream (DG1 mode)", ("k_keystream<16,2>: 1024 draws per lane, 128 lanes per "
+                                                          "1 MiB DG1 block, zero-prefix waves skip the PRNG")
     else:
+        batch = kind == "batch" or tiled
+        kernel = ("k_fill_batch" + (" (uniform tile records)" if tiled else "")) if batch else "k_fill_stream"
         waves = args.waves_per_block or (1 if batch else 2)
         launch_shape = (f"one {64 * waves}-thread workgroup per 4 KiB block, "
                         f"{ctx.query_occupancy(batch=batch)} resident per CU")
 
+    # per-launch HIP events on the launch stream (the single-buffer step is one group)
     def step(evs=None):
-        for L in launches:
+        for f, _ in launches:
             if evs is not None:
                 evs.append(torch.cuda.Event(enable_timing=True))
                 evs[-1].record(stream)
-            if L[0] == "keystream":
-                call("s3dg_xoshiro_fill", ctx._h, base_ptr, L[1], 2 * MiB, L[2], sh)
-            elif L[0] == "stream":
-                _, size, stride, k, first = L
-                call("s3dg_fill_controlled_stream", ctx._h, base_ptr, size, stride, k,
-                     cfg["dedup"], fn, fd, SEED_BASE, first, sh)
-            else:
-                call("s3dg_fill_controlled_batch", ctx._h, base_ptr, L[1], L[2], sh)
+            f()
             if evs is not None:
                 evs.append(torch.cuda.Event(enable_timing=True))
                 evs[-1].record(stream)
@@ -234,104 +339,58 @@ def main() -> int:
     t1 = time.perf_counter()
     elapsed = cp.max(t1 - t0)
     kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(0, len(evs), 2)]
-    launch_bytes = [step_bytes / len(launches)] * len(kern_ms)   # uniform split (exact for one launch)
-    if len(launches) > 1 and cfg["size"] is None:
-        per = [sum(L[1][k].size for k in range(L[2])) for L in launches]
-        launch_bytes = per * args.steps
-    elif len(launches) > 1:
-        per = [L[1] if L[0] == "keystream" else L[3] * L[1] for L in launches]
-        launch_bytes = per * args.steps
+    launch_bytes = [b for _, b in launches] * args.steps
     avg_ms = sum(kern_ms) / len(kern_ms)
     achieved_gbs = sum(launch_bytes) / (sum(kern_ms) * 1e-3) / 1e9
+    if kind == "single":                       # one "launch" = one call
+        avg_ms /= launches[0][1] // cfg["size"]
+    algo_per_launch = int(sum(launch_bytes) / len(launch_bytes))
+    if kind == "single":
+        algo_per_launch = cfg["size"]
 
     total_bytes = cp.sum(step_bytes) * args.steps
     value = total_bytes / elapsed / GiB
 
-    # ---- verification: sampled ring slots vs the C oracle -------------------------------
+    # ---- verification: sampled objects of the last writes vs the C oracle ---------------
     verified = None
     if not args.no_verify:
-        from oracle import oracle_c as OC
-        import random
-        base = OC.base_block(BASE_SEED)
-        slots = sorted(slot_obj)
-        rnd = random.Random(1234 + rank)
-        pick = {slots[0], slots[-1]} | set(rnd.sample(slots, min(16, len(slots))))
-        ok = True
-        for s in sorted(pick):
-            j, size, off = slot_obj[s]
-            if cfg.get("keystream"):
-                last = launches[-1]
-                chunk0 = last[2] + s * 4           # 4 x 2 MiB chunks per 8 MiB slot
-                got = ring[off:off + 2 * MiB].cpu().numpy()
-                exp = OC.xoshiro_chunks(2 * MiB, 2 * MiB, chunk0)
-                ok &= sha(got) == sha(exp)
-                continue
-            got = ring[off:off + size].cpu().numpy()
-            exp = OC.fill_controlled(size, cfg["dedup"], fn, fd, object_entropy(SEED_BASE, j), base)
-            ok &= sha(got) == sha(exp)
-        verified = bool(cp.max(0.0 if ok else 1.0) == 0.0)
-        if not verified:
-            print("bench: VERIFICATION FAILED: sampled objects differ from the oracle", file=sys.stderr)
+        verified = verify(torch, ring, samples, cfg, fn, fd, rank, cp)
 
-    # ---- write-only ceiling on the same buffer -----------------------------------------
-    # a store-only kernel (one 4 KiB chunk per workgroup, 16-byte stores) in the
-    # stream fill kernel's launch shape and in the shapes that measured fastest
-    # for pure stores on MI355X (tools/batch_lab.py); the largest is the ceiling
-    ceil_bytes = min(int(ring.numel()), 16 * GiB) // 4096 * 4096
-
-    def ceiling_rate(fn=None):
-        fn = fn or ctx.write_ceiling
-        fn(ring, ceil_bytes, stream=stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(3):
-            fn(ring, ceil_bytes, stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        return 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    ceil_shapes = {}
-    names = {-1: "default", 0: "plain", 1: "nt", 2: "sc1", 3: "ntsc1"}
-    for waves, occ, sp in [(args.waves_per_block or 2, -1 if args.occupancy is None else args.occupancy, store),
-                           (4, 4, 2), (4, 3, 2), (2, 4, 2), (4, 0, 0), (4, 4, 0)]:
-        ctx.set_waves_per_block(waves)
+    # ---- write ceilings on the same buffer ----------------------------------------------
+    ceil = None
+    if not args.no_ceiling and kind in ("stream", "batch", "keystream"):
+        ceil = ceilings(torch, ctx, ring, stream, args, store)
+        ctx.set_waves_per_block(args.waves_per_block or 0)
+        occ = -1 if args.occupancy is None else args.occupancy
         ctx.set_occupancy(occ, occ)
-        ctx.set_store_policy(sp, sp)
-        ceil_shapes[f"{waves}w_{ctx.query_occupancy()}perCU_{names[sp]}"] = round(ceiling_rate(), 1)
-    # the tiled fill's shape: batch knobs (1 wave, uncapped, sc1) + trailing record loads
-    ctx.set_waves_per_block(args.waves_per_block or 0)
-    ctx.set_occupancy(-1 if args.occupancy is None else args.occupancy, -1 if args.occupancy is None else args.occupancy)
-    ctx.set_store_policy(store, store)
-    ceil_shapes[f"tiled_1w_{ctx.query_occupancy(batch=True)}perCU_{names[store]}"] = round(
-        ceiling_rate(ctx.write_ceiling_tiled), 1)
-    # the runtime's own fill (SURVEY.md §8d names it as a ceiling option)
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemsetD32Async.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
-
-    def memset_d32(buf, nbytes, stream):
-        sh = int(getattr(stream, "cuda_stream", stream or 0))
-        assert hip.hipMemsetD32Async(buf.data_ptr(), 0x5A5A5A5A, nbytes // 4, sh) == 0
-    ceil_shapes["hipMemsetD32Async"] = round(ceiling_rate(memset_d32), 1)
-    ceiling_gbs = max(ceil_shapes.values())
-    ctx.set_waves_per_block(args.waves_per_block or 0)
-    occ = -1 if args.occupancy is None else args.occupancy
-    ctx.set_occupancy(occ, occ)
+        ctx.set_store_policy(store, store)
 
     # ---- D2H-inclusive rate (bounded sample; never `value`) -------------------------------
     d2h = None
-    if not args.no_d2h and cfg["size"] is not None:
-        d2h = d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo)
+    if not args.no_d2h and kind in ("stream", "keystream", "dgen"):
+        reps = [d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo) for _ in range(max(1, args.d2h_reps))]
+        d2h = reps[-1]
+        if len(reps) > 1:
+            d2h["all_samples_GiBps"] = [r["value"] for r in reps]
         # every rank measures at the same time: the aggregate is what the node moves
         d2h["aggregate_all_ranks"] = round(cp.sum(d2h["value"]), 2)
 
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg.get("keystream"):
-        if cfg["size"] is not None:
-            cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds)
-        else:
-            cpu = cpu_baseline_batch(cfg, fn, fd, args.cpu_seconds, sizes)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes)
 
     if rank == 0:
+        roof = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic_from_profiles(args.config, algo_per_launch),
+                "kernel": kernel, "launch_shape": launch_shape,
+                "avg_launch_ms": round(avg_ms, 4),
+                "algorithmic_bytes_per_launch": algo_per_launch,
+                "source_digest": source_digest()}
+        if ceil:
+            roof.update(ceil)
+            roof["frac_of_write_ceiling"] = round(achieved_gbs / ceil["write_ceiling_GBps"], 4)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -347,21 +406,13 @@ def main() -> int:
             "data": "synthetic (seeded: seed_base=0x5EED000000000001, base block seed 0xBA5EB10C00000000)",
             "config": {"workload": cfg["name"], "objects_per_rank": n_rank,
                        "bytes_per_step_all_ranks": int(total_bytes // args.steps),
-                       "dedup": cfg["dedup"], "compress": list(cfg["compress"]) if isinstance(cfg["compress"], tuple) else cfg["compress"],
+                       "dedup": d, "compress": list(cfg["compress"]) if isinstance(cfg["compress"], tuple)
+                       else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
                        "stores": (args.store if args.store != "default"
-                                  else ("sc1" if batch else "nt sc1"))},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                         "traffic": traffic_from_profiles(args.config, int(sum(launch_bytes) / len(launch_bytes))),
-                         "kernel": "k_keystream" if cfg.get("keystream") else (
-                             "k_fill_batch" + (" (uniform tile records)" if tiled else "") if batch else "k_fill_stream"),
-                         "launch_shape": launch_shape,
-                         "avg_launch_ms": round(avg_ms, 3),
-                         "algorithmic_bytes_per_launch": int(sum(launch_bytes) / len(launch_bytes)),
-                         "write_ceiling_GBps": round(ceiling_gbs, 1),
-                         "write_ceiling_shapes_GBps": ceil_shapes,
-                         "frac_of_write_ceiling": round(achieved_gbs / ceiling_gbs, 4)},
+                                  else {"keystream": "sc1", "dgen": "plain"}.get(kind, "sc1" if kind == "batch"
+                                                                                  or tiled else "nt sc1"))},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "d2h_inclusive": d2h,
             "verified_vs_oracle": verified,
@@ -371,27 +422,125 @@ def main() -> int:
     return 0
 
 
+def verify(torch, ring, samples, cfg, fn, fd, rank, cp) -> bool:
+    """The first, the last and 16 random samples of the step's last writes,
+    byte for byte against the C oracle."""
+    import random
+    from oracle import oracle_c as OC
+    base = OC.base_block(BASE_SEED)
+    rnd = random.Random(1234 + rank)
+    idx = sorted({0, len(samples) - 1} | set(rnd.sample(range(len(samples)), min(16, len(samples)))))
+    ok = True
+    for i in idx:
+        off, what = samples[i]
+        if what[0] == "chunk":                  # 2 MiB keystream chunk
+            got = ring[off:off + 2 * MiB].cpu().numpy()
+            ok &= sha(got) == sha(OC.xoshiro_chunks(2 * MiB, 2 * MiB, what[1]))
+        elif what[0] == "obj":
+            _, j, size = what
+            got = ring[off:off + size].cpu().numpy()
+            exp = OC.fill_controlled(size, cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, j), base)
+            ok &= sha(got) == sha(exp)
+        elif what[0] == "single":
+            got = ring[:what[1]].cpu().numpy()
+            ok &= sha(got) == sha(OC.fill_controlled(what[1], cfg["dedup"], fn, fd, 7, base))
+        else:                                   # DG1: block 0 of the object (1 MiB)
+            got = ring[off:off + MiB].cpu().numpy()
+            exp = OC.dgen_fill(MiB, cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, what[1]))
+            ok &= sha(got) == sha(exp)
+    verified = bool(cp.max(0.0 if ok else 1.0) == 0.0)
+    if not verified:
+        print("bench: VERIFICATION FAILED: sampled objects differ from the oracle", file=sys.stderr)
+    return verified
+
+
+def ceilings(torch, ctx, ring, stream, args, store) -> dict:
+    """Store-only references on the same buffer (<= 16 GiB).  The ceiling the
+    fill is judged against is its own launch with the PRNG chain and the
+    window patches compiled out (s3dg_write_ceiling_fill: same records, grid,
+    LDS image, barrier, stores and trailing loads); the other shapes are kept
+    for comparison (pure store kernels overdrive the L2's
+    write path and run slower than the fill)."""
+    ceil_bytes = min(int(ring.numel()), 16 * GiB) // (8 * MiB) * (8 * MiB)
+    if ceil_bytes == 0:
+        return {}
+
+    def rate(fn):
+        fn(ring, ceil_bytes, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            fn(ring, ceil_bytes, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return 3 * ceil_bytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    ctx.set_waves_per_block(args.waves_per_block or 0)
+    occ = -1 if args.occupancy is None else args.occupancy
+    ctx.set_occupancy(occ, occ)
+    ctx.set_store_policy(store, store)
+    fill_ceiling = round(rate(ctx.write_ceiling_fill), 1)
+    shapes = {}
+    names = {-1: "default", 0: "plain", 1: "nt", 2: "sc1", 3: "ntsc1"}
+    shapes[f"tiled_1w_{ctx.query_occupancy(batch=True)}perCU_{names[store]}"] = round(
+        rate(ctx.write_ceiling_tiled), 1)
+    for waves, occ_, sp in [(4, 4, 2), (2, 4, 2), (4, 0, 0)]:
+        ctx.set_waves_per_block(waves)
+        ctx.set_occupancy(occ_, occ_)
+        ctx.set_store_policy(sp, sp)
+        shapes[f"{waves}w_{ctx.query_occupancy()}perCU_{names[sp]}"] = round(rate(ctx.write_ceiling), 1)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemsetD32Async.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+
+    def memset_d32(buf, nbytes, stream):
+        assert hip.hipMemsetD32Async(buf.data_ptr(), 0x5A5A5A5A, nbytes // 4, int(stream.cuda_stream)) == 0
+    shapes["hipMemsetD32Async"] = round(rate(memset_d32), 1)
+    return {"write_ceiling_GBps": fill_ceiling,
+            "write_ceiling_kind": "k_fill_batch with the PRNG chain and window patches compiled out "
+                                  "(s3dg_write_ceiling_fill), 8 MiB objects",
+            "store_only_shapes_GBps": shapes}
+
+
 def traffic_from_profiles(config: int, launch_bytes: int):
-    """HBM bytes per launch from the committed PMC pass (profiles/traffic.json),
-    only when it was taken on this exact config and launch size."""
+    """HBM bytes per launch from the committed PMC passes (profiles/traffic.json),
+    only when they were taken on this config, this launch size and this
+    library source (source_digest)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(p) as f:
             t = json.load(f).get(str(config))
-        if t and t.get("algorithmic_bytes_per_launch") == launch_bytes:
+        if (t and t.get("algorithmic_bytes_per_launch") == launch_bytes
+                and t.get("source_digest") == source_digest()):
             return t.get("traffic_bytes_per_launch")
     except Exception:
         pass
     return None
 
 
-def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=1024, per_chunk=32):
-    """Generate n_objs objects through two device chunk buffers and copy each
-    chunk to a pinned host ring on the GPU's NUMA node, on a second stream
-    (the PUT path's input)."""
-    import ctypes
+def numa_of(ptr: int) -> dict:
+    """NUMA placement of the mapping holding `ptr` (/proc/self/numa_maps:
+    pages per node of the mapping that starts at or below ptr)."""
+    best, line = -1, ""
+    try:
+        for l in open("/proc/self/numa_maps"):
+            a = int(l.split()[0], 16)
+            if best < a <= ptr:
+                best, line = a, l
+    except Exception:
+        return {}
+    return {k: int(v) for k, v in (f.split("=") for f in line.split() if f[:1] == "N" and "=" in f)}
+
+
+def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=256 * MiB):
+    """Generate `total` bytes of the config's objects through two device chunk
+    buffers and copy each chunk to a pinned host ring on the GPU's NUMA node,
+    on a second stream (the PUT path's input).  Logs where the ring's pages
+    are, the CPUs the process runs on and the per-copy rates (HIP events on
+    the copy stream), so run-to-run spread can be attributed."""
+    kind = cfg["kind"]
     size = cfg["size"]
-    cb = per_chunk * size
+    per_chunk = max(1, chunk // size) if kind != "dgen" else 1
+    cb = per_chunk * size if kind != "dgen" else chunk
+    nchunks = total // cb
     gen = torch.cuda.Stream(device=dev)
     cpy = torch.cuda.Stream(device=dev)
     devbuf = [torch.empty(cb, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(2)]
@@ -404,74 +553,157 @@ def d2h_inclusive(torch, ctx, lib, call, dev, cfg, fn, fd, lo, n_objs=1024, per_
     call("s3dg_device_numa_node", dev, ctypes.byref(node))
     gen_done = [torch.cuda.Event() for _ in range(2)]
     cpy_done = [torch.cuda.Event() for _ in range(2)]
+    cev = []
 
-    def run(n):
-        for k in range(n // per_chunk):
+    def run(n, timed):
+        for k in range(n):
             s = k & 1
             gen.wait_event(cpy_done[s])
-            call("s3dg_fill_controlled_stream", ctx._h, int(devbuf[s].data_ptr()), size, size,
-                 per_chunk, cfg["dedup"], fn, fd, SEED_BASE, lo + k * per_chunk,
-                 int(gen.cuda_stream))
+            if kind == "keystream":
+                call("s3dg_xoshiro_fill", ctx._h, int(devbuf[s].data_ptr()), cb, 2 * MiB,
+                     (lo * size + k * cb) // (2 * MiB), int(gen.cuda_stream))
+            elif kind == "dgen":
+                call("s3dg_dgen_fill", ctx._h, int(devbuf[s].data_ptr()), size, k * (cb >> 20),
+                     (k + 1) * (cb >> 20), cfg["dedup"], fn, fd, SEED_BASE, int(gen.cuda_stream))
+            else:
+                call("s3dg_fill_controlled_stream", ctx._h, int(devbuf[s].data_ptr()), size, size,
+                     per_chunk, cfg["dedup"], fn, fd, SEED_BASE, lo + k * per_chunk, int(gen.cuda_stream))
             gen_done[s].record(gen)
             cpy.wait_event(gen_done[s])
+            if timed:
+                cev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                cev[-1][0].record(cpy)
             call("s3dg_d2h_async", ctx._h, host[s], int(devbuf[s].data_ptr()), cb, int(cpy.cuda_stream))
+            if timed:
+                cev[-1][1].record(cpy)
             cpy_done[s].record(cpy)
     try:
         for s in range(2):
             cpy_done[s].record(cpy)
-        run(n_objs // 2)          # the first GiBs into fresh pinned pages copy slower
+        run(max(2, nchunks // 4), False)          # the first GiBs into fresh pinned pages copy slower
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run(n_objs)
+        run(nchunks, True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        pages = [numa_of(p) for p in host]
     finally:
         torch.cuda.synchronize()
         for p in host:
             call("s3dg_host_free_pinned", p)
-    return {"value": round(n_objs * size / dt / GiB, 2), "unit": "GiB/s",
-            "sample": f"{n_objs} x {size // MiB} MiB objects, 2 x {per_chunk}-object device chunks, "
-                      f"pinned host ring on NUMA node {node.value}, generate || D2H on two streams"}
+    rates = sorted(cb / (a.elapsed_time(b) * 1e-3) / GiB for a, b in cev)
+    cpus = sorted(os.sched_getaffinity(0))
+    cpu_nodes = set()
+    for nd in os.listdir("/sys/devices/system/node") if os.path.isdir("/sys/devices/system/node") else []:
+        if nd.startswith("node"):
+            try:
+                from_list = open(f"/sys/devices/system/node/{nd}/cpulist").read().strip()
+                ids = set()
+                for part in from_list.split(","):
+                    a, _, b = part.partition("-")
+                    ids.update(range(int(a), int(b or a) + 1))
+                if ids & set(cpus):
+                    cpu_nodes.add(int(nd[4:]))
+            except Exception:
+                pass
+    return {"value": round(nchunks * cb / dt / GiB, 2), "unit": "GiB/s",
+            "sample": f"{nchunks} x {cb // MiB} MiB device chunks ({nchunks * cb // GiB} GiB) of the config's "
+                      f"objects, 2 device chunks, pinned host ring (hipHostMalloc default flags, allocated from a "
+                      f"thread bound to the GPU's local CPUs), generate || D2H on two streams",
+            "gpu_numa_node": node.value, "ring_pages_per_node": pages,
+            "process_cpu_nodes": sorted(cpu_nodes),
+            "copy_GiBps_min_med_max": [round(rates[0], 1), round(rates[len(rates) // 2], 1), round(rates[-1], 1)]}
 
 
-def cpu_baseline_batch(cfg, fn, fd, seconds, sizes):
-    """Mixed-size configs: the C restatement per object (s3dgo_fill_controlled),
-    objects spread over a pool of host threads.  Each thread writes its objects
-    one after another into its own 256 MiB host ring (wrapping), so the bytes
-    stream to DRAM as the GPU's do to HBM instead of staying in the caches."""
-    import ctypes
+def object_entropy_py(seed_base: int, j: int) -> int:
+    return (seed_base + (j << 32)) & (2**64 - 1)
+
+
+def cpu_baseline(cfg, fn, fd, seconds, sizes):
+    """The C restatement of the same generator (oracle, kind 'port') on this
+    host's cores, parallel like the reference's Rayon loops.  Bounded sample
+    (~`seconds` of CPU time) into reused host memory."""
     import threading
     import numpy as np
     from oracle import oracle_c as OC
-    threads = max(1, min(16, os.cpu_count() or 1))
+    share = cpu_share()
+    threads = share["threads"]
     base = OC.base_block(BASE_SEED)
+    kind = cfg["kind"]
+    meta = {"cores": threads, "kind": "port", "affinity_cpus": share["affinity_cpus"],
+            "cgroup_quota_cpus": share["cgroup_quota_cpus"]}
+    if kind in ("stream", "single"):
+        # fill_controlled_data's par_chunks_mut(4096) over a reused 1 GiB ring
+        size = cfg["size"]
+        per = max(1, GiB // size)
+        buf = np.ones(per * size, np.uint8)                        # fault the pages in before timing
+        OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, 0, base, threads=threads, out=buf)
+        done, t0, k = 0, time.perf_counter(), 0
+        while True:
+            OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, k * per, base, threads=threads, out=buf)
+            done += per
+            k += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds:
+                break
+        t1s = time.perf_counter()
+        OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, 0, base, threads=1, out=buf)
+        one = per * size / (time.perf_counter() - t1s) / GiB
+        return dict(meta, value=round(done * size / dt / GiB, 2), unit="GiB/s", single_thread_GiBps=round(one, 2),
+                    sample=f"{done} x {size // KiB} KiB objects ({done * size / GiB:.0f} GiB) over {dt:.1f} s into "
+                           f"a reused 1 GiB host ring, {threads} threads over 4 KiB blocks; {cpu_model()}")
+    # per-object (or per-chunk) tasks from a pool of host threads, each thread
+    # writing its own reused host ring
     L = OC.lib()
-    ring = max(256 * MiB, max(sizes))
+    if kind == "batch":
+        ring = max(256 * MiB, max(sizes))
+        items = sizes
+
+        def work(buf, pos, j):
+            sz = items[j % len(items)]
+            if pos + sz > ring:
+                pos = 0
+            L.s3dgo_fill_controlled(ctypes.cast(buf.ctypes.data + pos, ctypes.POINTER(ctypes.c_uint8)), sz,
+                                    cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, j),
+                                    base.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+            return pos + (sz + 4095) // 4096 * 4096, sz
+        what = "objects of the config's sizes, one object per task"
+    elif kind == "keystream":
+        ring = 256 * MiB
+
+        def work(buf, pos, j):
+            if pos + 2 * MiB > ring:
+                pos = 0
+            OC.xoshiro_chunks(2 * MiB, 2 * MiB, j, out=buf[pos:pos + 2 * MiB])
+            return pos + 2 * MiB, 2 * MiB
+        what = "2 MiB keystream chunks (npz.rs:376-383), one chunk per task"
+    else:   # dgen: 8 MiB pieces of DG1 objects
+        ring = 256 * MiB
+
+        def work(buf, pos, j):
+            if pos + 8 * MiB > ring:
+                pos = 0
+            OC.dgen_fill(8 * MiB, cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, j), out=buf[pos:pos + 8 * MiB])
+            return pos + 8 * MiB, 8 * MiB
+        what = "8 MiB DG1 objects, one object per task"
     lock = threading.Lock()
-    state = {"next": 0, "bytes": 0, "objs": 0, "stop": False}
+    state = {"next": 0, "bytes": 0, "tasks": 0, "stop": False}
     start = threading.Event()
 
     def worker():
-        buf = np.ones(ring, np.uint8)                     # faulted in before timing starts
-        addr = buf.ctypes.data
-        pp = base.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
-        done = nobj = pos = 0
+        buf = np.ones(ring, np.uint8)
+        done = ntask = pos = 0
         start.wait()
         while not state["stop"]:
             with lock:
                 j = state["next"]
                 state["next"] += 1
-            sz = sizes[j % len(sizes)]
-            if pos + sz > ring:
-                pos = 0
-            L.s3dgo_fill_controlled(ctypes.cast(addr + pos, ctypes.POINTER(ctypes.c_uint8)), sz, cfg["dedup"],
-                                    fn, fd, object_entropy_py(SEED_BASE, j), pp)
-            pos += (sz + 4095) // 4096 * 4096
-            done += sz
-            nobj += 1
+            pos, b = work(buf, pos, j)
+            done += b
+            ntask += 1
         with lock:
             state["bytes"] += done
-            state["objs"] += nobj
+            state["tasks"] += ntask
     ts = [threading.Thread(target=worker) for _ in range(threads)]
     for t in ts:
         t.start()
@@ -483,53 +715,9 @@ def cpu_baseline_batch(cfg, fn, fd, seconds, sizes):
     for t in ts:
         t.join()
     dt = time.perf_counter() - t0
-    try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
-    except Exception:
-        model = "unknown"
-    return {"value": round(state["bytes"] / dt / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{state['objs']} objects of the config's sizes ({state['bytes'] / GiB:.0f} GiB) over "
-                      f"{dt:.1f} s, one object per task on {threads} threads, each thread writing a "
-                      f"{ring // MiB} MiB host ring; {model}"}
-
-
-def object_entropy_py(seed_base: int, j: int) -> int:
-    return (seed_base + (j << 32)) & (2**64 - 1)
-
-
-def cpu_baseline(cfg, fn, fd, seconds):
-    """The C restatement (oracle, kind='port') on this host's cores, like the
-    reference's Rayon par_chunks_mut(4096) (src/data_gen.rs:198)."""
-    import numpy as np
-    from oracle import oracle_c as OC
-    threads = max(1, min(16, os.cpu_count() or 1))
-    size = cfg["size"]
-    per = max(1, (1 * GiB) // size)            # 1 GiB host ring, reused
-    buf = np.zeros(per * size, np.uint8)
-    buf[:] = 1                                   # fault the pages in before timing
-    base = OC.base_block(BASE_SEED)
-    OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, 0, base, threads=threads, out=buf)
-    done, t0, k = 0, time.perf_counter(), 0
-    while True:
-        OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, k * per, base,
-                       threads=threads, out=buf)
-        done += per
-        k += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    t1s = time.perf_counter()
-    OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, 0, base, threads=1, out=buf)
-    one = per * size / (time.perf_counter() - t1s) / GiB
-    try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
-    except Exception:
-        model = "unknown"
-    return {"value": round(done * size / dt / GiB, 2), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{done} x {size // MiB} MiB objects ({done * size / GiB:.0f} GiB) over "
-                      f"{dt:.1f} s into a reused 1 GiB host ring; {model}",
-            "single_thread_GiBps": round(one, 2)}
+    return dict(meta, value=round(state["bytes"] / dt / GiB, 2), unit="GiB/s",
+                sample=f"{state['tasks']} {what} ({state['bytes'] / GiB:.0f} GiB) over {dt:.1f} s on {threads} "
+                       f"threads, each writing a {ring // MiB} MiB host ring; {cpu_model()}")
 
 
 if __name__ == "__main__":

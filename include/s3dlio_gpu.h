@@ -58,6 +58,7 @@ typedef struct {
 /* ---- context ------------------------------------------------------------ */
 int s3dg_ctx_create(int device, s3dg_ctx **out);
 int s3dg_ctx_destroy(s3dg_ctx *ctx);
+int s3dg_ctx_device(s3dg_ctx *ctx, int *device);
 /* Replace the 4 KiB base block (stands in for A_BASE_BLOCK,
  * src/constants.rs:715-720).  Host pointer, 4096 bytes. */
 int s3dg_set_base_block(s3dg_ctx *ctx, const uint8_t *base4096);
@@ -82,8 +83,10 @@ int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_c
  * the L2 with later tile records; 0 = off, UINT32_MAX = default (256).
  * Results are identical. */
 int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
-/* Batch launches: blocks per tile record (8, 16, 32 or 64); 0 = chosen per
- * launch from the object sizes (default).  Results are identical. */
+/* Batch launches: blocks per tile record (8, 16, 32 or 64), 1 = dense (one
+ * record per 4 KiB granule of the batch's address range; used only when
+ * the objects are 4 KiB-aligned, sorted and non-overlapping); 0 = chosen per
+ * sub-batch by cost (default).  Results are identical. */
 int s3dg_set_batch_tile(s3dg_ctx *ctx, uint32_t blocks);
 /* 1 = run large uniform streams (>= 64 MiB, objects 32 KiB-aligned relative
  * to each other) through the tiled batch kernel with device-built tile
@@ -133,7 +136,10 @@ int s3dg_fill_controlled_stream(s3dg_ctx *ctx, void *dst, uint64_t obj_size,
                                 uint64_t stride, uint64_t n_objs, uint64_t dedup,
                                 uint32_t f_num, uint32_t f_den, uint64_t seed_base,
                                 uint64_t first_obj, void *stream);
-/* Mixed-size batch.  `descs` is a host array; it is copied before return. */
+/* Mixed-size batch.  `descs` is a host array; it is consumed before return
+ * (in sub-batches whose preparation overlaps the previous sub-batch's fill).
+ * Descriptors are checked per sub-batch: when one is invalid the call fails
+ * and the objects of earlier sub-batches may already be enqueued. */
 int s3dg_fill_controlled_batch(s3dg_ctx *ctx, void *dst_base,
                                const s3dg_obj_desc *descs, uint64_t n, void *stream);
 /* Keystream fill (generate_npz_bytes_raw x-fill, src/data_formats/npz.rs:376-383):
@@ -161,6 +167,13 @@ int s3dg_write_ceiling(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern,
  * the context's tile-map records, as k_fill_batch): the ceiling for tiled
  * batches and streams. */
 int s3dg_write_ceiling_tiled(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pattern, void *stream);
+/* The store-only reference of the tiled fill itself: the launch
+ * s3dg_fill_controlled_stream makes for len bytes of 8 MiB objects (same
+ * tile records, grid, LDS image, barrier, stores and trailing record loads)
+ * with the PRNG chain and the window patches compiled out.  Its bytes are
+ * meaningless; it is the write ceiling the fill is measured against.
+ * len < 8 MiB or a multiple of 8 MiB. */
+int s3dg_write_ceiling_fill(s3dg_ctx *ctx, void *dst, uint64_t len, void *stream);
 
 /* ---- memory / copy helpers ------------------------------------------------ */
 int s3dg_device_alloc(s3dg_ctx *ctx, uint64_t bytes, void **out);
@@ -196,8 +209,8 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
                    uint64_t num_samples, uint8_t *out, uint64_t out_len);
 
 /* ---- streaming generator (DataGenerator / ObjectGen / PyO3 Generator) ----- */
-/* One object of `size` bytes in the DG1 layout, generated on the default
- * context's GPU and streamed into host buffers.  has_seed=0: time + counter
+/* One object of `size` bytes in the DG1 layout, generated on a host slot's
+ * GPU (taken round-robin at creation) and streamed into host buffers.  has_seed=0: time + counter
  * entropy like DataGenerator::new(None) (src/data_gen.rs:271-291).
  * compress/dedup 0 are treated as 1 (src/data_gen_alt.rs:108-109). */
 typedef struct s3dg_gen s3dg_gen;
@@ -215,6 +228,8 @@ int s3dg_gen_is_complete(s3dg_gen *gen);
 uint64_t s3dg_gen_position(s3dg_gen *gen);
 uint64_t s3dg_gen_total_size(s3dg_gen *gen);
 uint64_t s3dg_gen_seed(s3dg_gen *gen);
+/* The host slot the generator runs on (s3dg_host_slot_device gives its GPU). */
+int s3dg_gen_slot(s3dg_gen *gen);
 int s3dg_gen_reset(s3dg_gen *gen);
 /* generate_data / generate_controlled_data_alt one-shot into buf. */
 int s3dg_generate_data(uint8_t *buf, uint64_t size, uint64_t dedup, uint64_t compress,
@@ -282,16 +297,33 @@ int s3dg_put_objects_multi(s3dg_ctx *const *ctxs, uint32_t nctx, const char *con
                            uint32_t *crc_out, s3dg_put_stats *stats);
 
 /* ---- host-buffer drop-ins (src/data_gen.rs:151 signature) ---------------- */
+/* The host-buffer entry points (s3dlio_*, s3dg_gen_*, s3dg_generate_data,
+ * s3dg_generate_object) run on a pool of SLOTS: one per GPU by default, each
+ * with its own context, base-block copies and staging sets.  Every call takes
+ * a slot round-robin (a generator keeps its slot); calls on different slots
+ * run on different GPUs concurrently, and a call of >= 256 MiB is cut into
+ * one range per slot generated in parallel.  Bytes never depend on the slot.
+ * Slot devices: env S3DLIO_GPU_DEVICE=k pins every call to GPU k;
+ * S3DLIO_GPU_DEVICES=a,b,... lists them (repeats: several slots on one GPU);
+ * neither: every visible GPU. */
+/* The slot device list for the given env values and device count (pure
+ * function; no GPU needed).  *n <= cap entries written to out. */
+int s3dg_host_parse_devices(const char *pin, const char *list, int ndev, int *out, int cap, int *n);
+int s3dg_host_slot_count(int *out);
+int s3dg_host_slot_device(int slot, int *device);
+/* The slot's context (owned by the pool: never destroy it); slot < 0 takes
+ * the next slot round-robin. */
+int s3dg_host_slot_context(int slot, s3dg_ctx **out);
 /* generate_random_data(size) (src/data_gen.rs:102): seeded analogue layout
  * with time entropy and a per-process random BASE_BLOCK. */
 int s3dlio_generate_random_data(uint8_t *buf, size_t size);
 /* fill_controlled_data(buf, dedup, compress): time-based entropy and a
  * per-process random base block, exactly as the reference; generated on the
- * GPU of the process-default context (env S3DLIO_GPU_DEVICE, default 0) and
- * copied into `buf`.  Empty buffer: no-op. */
+ * host slots' GPUs (above) and copied into `buf`.  Empty buffer: no-op. */
 int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress);
 /* Seeded sibling: entropy replaces call_entropy; base4096 (nullable)
- * replaces A_BASE_BLOCK (NULL = the default context's base block). */
+ * replaces A_BASE_BLOCK (NULL = a context's default base block, seed
+ * 0xBA5EB10C00000000). */
 int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup,
                                        size_t compress, uint64_t entropy,
                                        const uint8_t *base4096);

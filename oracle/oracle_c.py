@@ -120,14 +120,15 @@ def fill_stream(obj_size: int, n: int, dedup: int, f_num: int, f_den: int,
     return out
 
 
-def xoshiro_chunks(length: int, chunk: int, seed_base: int) -> np.ndarray:
-    out = np.empty(length, np.uint8)
+def xoshiro_chunks(length: int, chunk: int, seed_base: int, out: np.ndarray | None = None) -> np.ndarray:
+    out = np.empty(length, np.uint8) if out is None else out
     lib().s3dgo_xoshiro_chunks(_ptr(out), length, chunk, seed_base)
     return out
 
 
-def dgen_fill(size: int, dedup: int, f_num: int, f_den: int, seed: int) -> np.ndarray:
-    out = np.empty(size, np.uint8)
+def dgen_fill(size: int, dedup: int, f_num: int, f_den: int, seed: int,
+              out: np.ndarray | None = None) -> np.ndarray:
+    out = np.empty(size, np.uint8) if out is None else out
     lib().s3dgo_dgen_fill(_ptr(out), size, dedup, f_num, f_den, seed & (2**64 - 1))
     return out
 

@@ -8,7 +8,8 @@ the library is absent (no CPU fallback exists).
 from ._lib import S3dgError, lib  # noqa: F401  (loads libs3dlio_amd.so)
 from .hostbuf import BytesView  # noqa: F401
 from .device import (BLOCK_SIZE, DEFAULT_BASE_SEED, Context, compress_ratio,  # noqa: F401
-                     device_count, object_entropy, unique_blocks, xoshiro_jump)
+                     device_count, host_context, host_slots, object_entropy, parse_devices,
+                     unique_blocks, xoshiro_jump)
 from .data_gen import fill_controlled_data, fill_controlled_data_seeded  # noqa: F401
 from .datagen import (DataGenerator, Generator, ObjectGen, default_data_gen_threads,  # noqa: F401
                       generate_controlled_data_alt, generate_controlled_data_streaming,

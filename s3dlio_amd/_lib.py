@@ -49,6 +49,7 @@ class PutStats(ctypes.Structure):
 SIGNATURES = {
     "s3dg_ctx_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "s3dg_ctx_destroy": (c_int, [c_vp]),
+    "s3dg_ctx_device": (c_int, [c_vp, ctypes.POINTER(c_int)]),
     "s3dg_set_base_block": (c_int, [c_vp, c_u8p]),
     "s3dg_set_base_block_seed": (c_int, [c_vp, c_u64]),
     "s3dg_get_base_block": (c_int, [c_vp, c_u8p]),
@@ -74,6 +75,7 @@ SIGNATURES = {
     "s3dg_fill_controlled_batch": (c_int, [c_vp, c_vp, ctypes.POINTER(ObjDesc), c_u64, c_vp]),
     "s3dg_write_ceiling": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
     "s3dg_write_ceiling_tiled": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
+    "s3dg_write_ceiling_fill": (c_int, [c_vp, c_vp, c_u64, c_vp]),
     "s3dg_xoshiro_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_vp]),
     "s3dg_xoshiro_jump": (c_int, [ctypes.POINTER(c_u64), c_u64]),
     "s3dg_dgen_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),
@@ -88,6 +90,12 @@ SIGNATURES = {
     "s3dg_gen_total_size": (c_u64, [c_vp]),
     "s3dg_gen_seed": (c_u64, [c_vp]),
     "s3dg_gen_reset": (c_int, [c_vp]),
+    "s3dg_gen_slot": (c_int, [c_vp]),
+    "s3dg_host_parse_devices": (c_int, [ctypes.c_char_p, ctypes.c_char_p, c_int, ctypes.POINTER(c_int), c_int,
+                                        ctypes.POINTER(c_int)]),
+    "s3dg_host_slot_count": (c_int, [ctypes.POINTER(c_int)]),
+    "s3dg_host_slot_device": (c_int, [c_int, ctypes.POINTER(c_int)]),
+    "s3dg_host_slot_context": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "s3dg_generate_data": (c_int, [c_vp, c_u64, c_u64, c_u64, c_int, c_u64]),
     "s3dg_crc32": (c_int, [c_vp, c_vp, c_u64, c_vp, ctypes.POINTER(c_u32)]),
     "s3dg_crc32_combine": (c_u32, [c_u32, c_u32, c_u64]),

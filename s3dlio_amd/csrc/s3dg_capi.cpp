@@ -15,9 +15,6 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 }  // namespace s3dg
 #include "s3dlio_gpu.h"
 
-#include <sys/random.h>
-#include <time.h>
-
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -42,6 +39,25 @@ constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small
 // block, whole waves fall inside the prefix and skip the PRNG)
 constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 2, 0, kStorePlain}};
 
+// Launch state private to one stream: the tile-record map of tiled launches
+// and the batch-descriptor staging.  Launches on one stream are ordered by
+// the stream, so a launch may rewrite the map as soon as it is enqueued after
+// the previous one; launches on different streams share nothing and never
+// wait on each other.
+struct StreamState {
+    std::mutex mu;                     // one enqueuing thread per stream at a time
+    TileRec *tiles = nullptr;          // records (device), grown on demand
+    uint64_t tile_cap = 0;
+    hipStream_t up = nullptr;          // batch entry uploads (overlap the previous fill)
+    struct Stage {
+        BatchEnt *host = nullptr, *dev = nullptr;   // pinned staging / device copy
+        uint64_t cap = 0;
+        hipEvent_t uploaded = nullptr;  // host staging may be rewritten
+        hipEvent_t consumed = nullptr;  // device copy may be overwritten (k_batch_map done)
+    } stage[2];
+    int next = 0;
+};
+
 struct s3dg_ctx {
     int device = 0;
     int cus = 256;                     // compute units (sizes small keystream launches)
@@ -54,19 +70,14 @@ struct s3dg_ctx {
     int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
     uint32_t prefetch_tiles = kDefaultPrefetch;   // batch tile-record prefetch distance
     uint32_t tile_shift = 0;           // batch tile = 2^tile_shift blocks; 0 = per launch
+    bool tile_force_dense = false;     // batch: one record per 4 KiB granule when the layout allows
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
     uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
-    // batch descriptor table (device) + pinned staging, grown on demand
-    ObjEntry *tab_dev = nullptr;
-    ObjEntry *tab_host = nullptr;
-    uint64_t tab_cap = 0;
-    TileRec *tile_obj = nullptr;       // per-tile records (device)
-    uint64_t tile_cap = 0;
-    hipEvent_t tab_free = nullptr;     // staging may be rewritten once this fires
-    hipEvent_t tile_free = nullptr;    // tile map may be rewritten once this fires
+    // tile maps and batch staging, one set per stream (s3dg::StreamState)
+    std::map<hipStream_t, StreamState *> streams;
     int stream_tiles = kDefaultStreamTiles;   // uniform streams through the tiled batch kernel
     std::map<uint64_t, uint64_t *> jtabs;   // (lpc << 32 | span) -> device jump table
     void *crc_tab = nullptr;           // slicing-by-8 tables (device)
@@ -125,22 +136,6 @@ constexpr uint64_t kDefaultBaseSeed = 0xBA5EB10C00000000ull;
     DeviceScope dscope_((c)->device);                                  \
     if (!dscope_.ok()) return hipfail(dscope_.err, "hipSetDevice")
 
-int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den,
-                PrefixParams *pp) {
-    if (f_den == 0) return fail(S3DG_EINVAL, "f_den must be >= 1");
-    if (f_num >= f_den) return fail(S3DG_EINVAL, "f_num must be < f_den (zero ratio < 1)");
-    if (nblocks > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
-    const uint64_t tot = (uint64_t)f_num * kBlk;
-    const uint64_t U = s3dg_unique_blocks(nblocks, dedup);
-    pp->unique = U == nblocks ? 0xFFFFFFFFu : (uint32_t)U;
-    pp->floor_len = (uint32_t)(tot / f_den);
-    pp->rem = (uint32_t)(tot % f_den);
-    pp->f_den = f_den;
-    pp->m_unique = fastmod_magic(pp->unique == 0xFFFFFFFFu ? 1u : pp->unique);
-    pp->m_fden = fastmod_magic(f_den);
-    return S3DG_OK;
-}
-
 LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false) {
     LaunchCfg lc;
     lc.store = batch ? c->store_batch : c->store_stream;
@@ -170,6 +165,38 @@ uint32_t pick_tile_shift(const uint64_t (&ntiles)[kTileShiftMax + 1]) {
 }
 
 }  // namespace
+
+namespace s3dg {
+
+int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                PrefixParams *pp) {
+    if (f_den == 0) return fail(S3DG_EINVAL, "f_den must be >= 1");
+    if (f_num >= f_den) return fail(S3DG_EINVAL, "f_num must be < f_den (zero ratio < 1)");
+    if (nblocks > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    const uint64_t tot = (uint64_t)f_num * kBlk;
+    const uint64_t U = s3dg_unique_blocks(nblocks, dedup);
+    pp->unique = U == nblocks ? 0xFFFFFFFFu : (uint32_t)U;
+    pp->floor_len = (uint32_t)(tot / f_den);
+    pp->rem = (uint32_t)(tot % f_den);
+    pp->f_den = f_den;
+    pp->m_unique = fastmod_magic(pp->unique == 0xFFFFFFFFu ? 1u : pp->unique);
+    pp->m_fden = fastmod_magic(f_den);
+    return S3DG_OK;
+}
+
+PrefixParams random_layout_prefix() {
+    PrefixParams pp{};
+    pp.unique = 0xFFFFFFFFu;            // block i seeded entropy + i
+    pp.f_den = 0;                       // generate_random_data layout
+    pp.m_unique = fastmod_magic(1);
+    pp.m_fden = fastmod_magic(1);
+    return pp;
+}
+
+LaunchCfg ctx_stream_cfg(const s3dg_ctx *c) { return cfg_for(const_cast<s3dg_ctx *>(c)); }
+const void *ctx_base(const s3dg_ctx *c) { return c->base_dev; }
+
+}  // namespace s3dg
 
 extern "C" {
 
@@ -215,10 +242,6 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
         c->cus = cus;
     hipError_t e = hipMalloc(&c->base_dev, kBlk);
     if (e != hipSuccess) { delete c; return hipfail(e, "hipMalloc(base block)"); }
-    e = hipEventCreateWithFlags(&c->tab_free, hipEventDisableTiming);
-    if (e != hipSuccess) { (void)hipFree(c->base_dev); delete c; return hipfail(e, "hipEventCreate"); }
-    e = hipEventCreateWithFlags(&c->tile_free, hipEventDisableTiming);
-    if (e != hipSuccess) { s3dg_ctx_destroy(c); return hipfail(e, "hipEventCreate"); }
     base_from_seed(kDefaultBaseSeed, c->base_host);
     e = hipMemcpy(c->base_dev, c->base_host, kBlk, hipMemcpyHostToDevice);
     if (e != hipSuccess) { s3dg_ctx_destroy(c); return hipfail(e, "hipMemcpy(base block)"); }
@@ -231,15 +254,28 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     DeviceScope ds(c->device);
     (void)hipDeviceSynchronize();
     if (c->base_dev) (void)hipFree(c->base_dev);
-    if (c->tab_dev) (void)hipFree(c->tab_dev);
-    if (c->tab_host) (void)hipHostFree(c->tab_host);
-    if (c->tile_obj) (void)hipFree(c->tile_obj);
+    for (auto &kv : c->streams) {
+        StreamState *S = kv.second;
+        if (S->tiles) (void)hipFree(S->tiles);
+        for (auto &G : S->stage) {
+            if (G.host) (void)hipHostFree(G.host);
+            if (G.dev) (void)hipFree(G.dev);
+            if (G.uploaded) (void)hipEventDestroy(G.uploaded);
+            if (G.consumed) (void)hipEventDestroy(G.consumed);
+        }
+        if (S->up) (void)hipStreamDestroy(S->up);
+        delete S;
+    }
     for (auto &kv : c->jtabs) (void)hipFree(kv.second);
     if (c->crc_tab) (void)hipFree(c->crc_tab);
     if (c->crc_seg) (void)hipFree(c->crc_seg);
-    if (c->tab_free) (void)hipEventDestroy(c->tab_free);
-    if (c->tile_free) (void)hipEventDestroy(c->tile_free);
     delete c;
+    return S3DG_OK;
+}
+
+int s3dg_ctx_device(s3dg_ctx *c, int *device) {
+    if (!c || !device) return fail(S3DG_EINVAL, "null argument");
+    *device = c->device;
     return S3DG_OK;
 }
 
@@ -306,12 +342,13 @@ int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
 int s3dg_set_batch_tile(s3dg_ctx *c, uint32_t blocks) {
     if (!c) return fail(S3DG_EINVAL, "null context");
     uint32_t sh = 0;
-    if (blocks != 0) {
+    if (blocks > 1) {
         while ((1u << sh) < blocks) ++sh;
         if ((1u << sh) != blocks || sh < kTileShiftMin || sh > kTileShiftMax)
-            return fail(S3DG_EINVAL, "tile blocks must be 0 (per launch), 8, 16, 32 or 64");
+            return fail(S3DG_EINVAL, "tile blocks must be 0 (per launch), 1 (dense), 8, 16, 32 or 64");
     }
     c->tile_shift = sh;
+    c->tile_force_dense = blocks == 1;
     return S3DG_OK;
 }
 
@@ -349,21 +386,26 @@ int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
     return S3DG_OK;
 }
 
-// The tile map (c->tile_obj) is shared by the context's batch and tiled
-// stream launches, which may be on different streams: grow it only once the
-// last launch reading it is done, and order the next k_tile_map after that
-// launch on the device (tile_free is recorded after every reader).  Caller
-// holds c->mu until it has recorded tile_free.
-static int tile_map_acquire(s3dg_ctx *c, uint64_t tiles, hipStream_t s) {
-    if (tiles > c->tile_cap) {
-        HIP_TRY(hipEventSynchronize(c->tile_free), "hipEventSynchronize(tile map)");
-        if (c->tile_obj) (void)hipFree(c->tile_obj);
-        c->tile_obj = nullptr; c->tile_cap = 0;
-        const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
-        HIP_TRY(hipMalloc(&c->tile_obj, cap * sizeof(TileRec)), "hipMalloc(tile map)");
-        c->tile_cap = cap;
-    }
-    HIP_TRY(hipStreamWaitEvent(s, c->tile_free, 0), "hipStreamWaitEvent(tile map)");
+// The stream's launch state (created on first use).
+static StreamState *stream_state(s3dg_ctx *c, hipStream_t s) {
+    std::lock_guard<std::mutex> g(c->mu);
+    StreamState *&S = c->streams[s];
+    if (!S) S = new StreamState();
+    return S;
+}
+
+// At least `tiles` records in the stream's map.  Earlier launches on this
+// stream may still read the old map: growing drains the stream first.
+// Caller holds S->mu.
+static int tiles_reserve(StreamState *S, uint64_t tiles, hipStream_t s) {
+    if (tiles <= S->tile_cap) return S3DG_OK;
+    HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize(tile map)");
+    if (S->tiles) (void)hipFree(S->tiles);
+    S->tiles = nullptr;
+    S->tile_cap = 0;
+    const uint64_t cap = tiles < 4096 ? 4096 : tiles + tiles / 4;
+    HIP_TRY(hipMalloc(&S->tiles, cap * sizeof(TileRec)), "hipMalloc(tile map)");
+    S->tile_cap = cap;
     return S3DG_OK;
 }
 
@@ -382,12 +424,12 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
             ntiles[sh] = n_objs * ((nb + lead + (1ull << sh) - 1) >> sh);
         const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
         const uint64_t tpo = (nb + lead + (1ull << tshift) - 1) >> tshift;
-        std::lock_guard<std::mutex> g(c->mu);
-        if (int r = tile_map_acquire(c, n_objs * tpo, s)) return r;
+        StreamState *S = stream_state(c, s);
+        std::lock_guard<std::mutex> g(S->mu);
+        if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
         HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
-                                          lead, seed_base + (first_obj << 32), pp, c->tile_obj, c->base_dev, s),
+                                          lead, seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s),
                 "launch k_fill_batch(stream)");
-        HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
         return S3DG_OK;
     }
     HIP_TRY(launch_fill_stream(cfg_for(c), dst, obj_size, stride, n_objs, 0, (uint32_t)nb, seed_base, first_obj,
@@ -425,11 +467,7 @@ int s3dg_random_data(s3dg_ctx *c, void *dst, uint64_t len, uint64_t entropy, voi
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
     const uint64_t nb = (len + kBlk - 1) / kBlk;
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
-    PrefixParams pp{};
-    pp.unique = 0xFFFFFFFFu;            // block i seeded entropy + i
-    pp.f_den = 0;                       // random-data layout
-    pp.m_unique = fastmod_magic(1);
-    pp.m_fden = fastmod_magic(1);
+    const PrefixParams pp = random_layout_prefix();
     return fill_uniform(c, (uint8_t *)dst, len, (len + 15) & ~15ull, 1, pp, entropy, 0, (hipStream_t)stream);
 }
 
@@ -456,10 +494,7 @@ int s3dg_internal_fill_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     PrefixParams pp{};
     if (random_layout) {
         if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
-        pp.unique = 0xFFFFFFFFu;
-        pp.f_den = 0;
-        pp.m_unique = fastmod_magic(1);
-        pp.m_fden = fastmod_magic(1);
+        pp = random_layout_prefix();
     } else if (int r = make_prefix(nb, dedup, f_num, f_den, &pp)) {
         return r;
     }
@@ -494,61 +529,137 @@ int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {
     return S3DG_OK;
 }
 
+// Mixed-size batch ("Batches"): the descriptors are cut into
+// sub-batches (16 Ki objects first, doubling to 256 Ki) so the host's two
+// passes over sub-batch k+1 overlap the GPU's fill of sub-batch k.  Per
+// sub-batch the host only validates, counts slots and writes 64-B BatchEnts
+// into pinned staging; the upload runs on the stream's side stream, and
+// k_batch_map derives prefix parameters and tile records on the device.
+// Record layout per sub-batch (cost model below):
+//   * tiles of 2^tshift blocks (8..64) per object, the object's block 0 at
+//     slot `lead` = its 4 KiB granule (mod 8): XCD-aligned, dead slots at
+//     both ends of every object;
+//   * dense (tshift 0): objects 4 KiB-aligned, sorted and non-overlapping;
+//     one record per 4 KiB granule of the sub-batch's address range, so slot
+//     = granule and only gaps are dead.
+// Descriptors are checked per sub-batch: on an error the objects of earlier
+// sub-batches may already be enqueued.
+constexpr uint64_t kBatchSubFirst = 16384, kBatchSubMax = 262144;
+// relative costs in units of one live 4 KiB block
+constexpr double kDeadSlotCost = 0.25, kRecordCost = 0.1;
+
 int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc *d, uint64_t n,
                                void *stream) {
     CTX_SCOPE(c);
     if (n == 0) return S3DG_OK;
     if (!d) return fail(S3DG_EINVAL, "null descriptor array");
     if (!dst_base || !aligned16(dst_base)) return fail(S3DG_EINVAL, "dst_base must be 16-byte aligned");
-    std::lock_guard<std::mutex> g(c->mu);
-    // the previous batch's upload must have left the pinned staging table
-    HIP_TRY(hipEventSynchronize(c->tab_free), "hipEventSynchronize");
-    if (n > c->tab_cap) {
-        if (c->tab_dev) (void)hipFree(c->tab_dev);
-        if (c->tab_host) (void)hipHostFree(c->tab_host);
-        c->tab_dev = nullptr; c->tab_host = nullptr; c->tab_cap = 0;
-        uint64_t cap = n < 1024 ? 1024 : n;
-        HIP_TRY(hipMalloc(&c->tab_dev, cap * sizeof(ObjEntry)), "hipMalloc(batch table)");
-        HIP_TRY(hipHostMalloc(&c->tab_host, cap * sizeof(ObjEntry), hipHostMallocDefault),
-                "hipHostMalloc(batch table)");
-        c->tab_cap = cap;
-    }
-    // Objects of size 0 contribute no tiles and no table entry.
-    uint64_t m = 0;
-    uint64_t ntiles[kTileShiftMax + 1] = {};
-    for (uint64_t k = 0; k < n; ++k) {
-        if (d[k].size == 0) continue;
-        if (d[k].dst_off & 15u) return fail(S3DG_EINVAL, "dst_off must be a multiple of 16");
-        const uint64_t nb = (d[k].size + kBlk - 1) / kBlk;
-        ObjEntry &e = c->tab_host[m++];
-        e.dst_off = d[k].dst_off;
-        e.size = d[k].size;
-        e.entropy = d[k].entropy;
-        // XCD alignment: slot (mod 8) = 4 KiB granule (mod 8) of the block's address
-        e.lead = (uint32_t)((((uintptr_t)dst_base + d[k].dst_off) >> 12) & 7);
-        e.pad = 0;
-        e.tile_begin = nb + e.lead;   // slot count until the tile size is known
-        if (int r = make_prefix(nb, d[k].dedup, d[k].f_num, d[k].f_den, &e.pp)) return r;
-        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
-            ntiles[sh] += (nb + e.lead + (1ull << sh) - 1) >> sh;
-    }
-    if (m == 0) return S3DG_OK;
-    const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
-    uint64_t tiles = 0;
-    for (uint64_t k = 0; k < m; ++k) {
-        const uint64_t slots = c->tab_host[k].tile_begin;
-        c->tab_host[k].tile_begin = tiles;
-        tiles += (slots + (1ull << tshift) - 1) >> tshift;
-    }
     hipStream_t s = (hipStream_t)stream;
-    if (int r = tile_map_acquire(c, tiles, s)) return r;
-    HIP_TRY(hipMemcpyAsync(c->tab_dev, c->tab_host, m * sizeof(ObjEntry), hipMemcpyHostToDevice, s),
-            "hipMemcpyAsync(batch table)");
-    HIP_TRY(hipEventRecord(c->tab_free, s), "hipEventRecord");
-    HIP_TRY(launch_fill_batch(cfg_for(c, true), (uint8_t *)dst_base, c->tab_dev, m, tiles, tshift,
-                              c->tile_obj, c->base_dev, s),
-            "launch k_fill_batch");
-    HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
+    const uintptr_t base = (uintptr_t)dst_base;
+    const LaunchCfg lc = cfg_for(c, true);
+    StreamState *S = stream_state(c, s);
+    std::lock_guard<std::mutex> g(S->mu);
+    if (!S->up) HIP_TRY(hipStreamCreateWithFlags(&S->up, hipStreamNonBlocking), "hipStreamCreate(upload)");
+    for (auto &G : S->stage)
+        for (hipEvent_t *ev : {&G.uploaded, &G.consumed})
+            if (!*ev) HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "hipEventCreate");
+    uint64_t sub = kBatchSubFirst;
+    for (uint64_t k0 = 0; k0 < n;) {
+        const uint64_t k1 = n - k0 < sub ? n : k0 + sub;
+        sub = sub * 2 < kBatchSubMax ? sub * 2 : kBatchSubMax;
+        // pass 1: validate, count slots per tile size, test the dense layout
+        uint64_t m = 0, blocks = 0, ntiles[kTileShiftMax + 1] = {};
+        uint64_t first_off = 0, prev_end = 0;
+        bool dense_ok = true;
+        for (uint64_t k = k0; k < k1; ++k) {
+            const s3dg_obj_desc &o = d[k];
+            if (o.size == 0) continue;
+            if (o.dst_off & 15u) return fail(S3DG_EINVAL, "dst_off must be a multiple of 16");
+            if (o.f_den == 0 || o.f_num >= o.f_den) return fail(S3DG_EINVAL, "need f_num < f_den");
+            const uint64_t nb = (o.size + kBlk - 1) / kBlk;
+            if (nb >= (1ull << 31)) return fail(S3DG_EINVAL, "object larger than 2^31 blocks");
+            const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
+            for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
+                ntiles[sh] += (nb + lead + (1ull << sh) - 1) >> sh;
+            if (m == 0) first_off = o.dst_off;
+            else if (o.dst_off < prev_end) dense_ok = false;
+            if (o.dst_off & (kBlk - 1)) dense_ok = false;
+            prev_end = o.dst_off + nb * kBlk;
+            blocks += nb;
+            ++m;
+        }
+        if (m == 0) { k0 = k1; continue; }
+        const uint64_t lead0 = ((base + first_off) >> 12) & 7;
+        const uint64_t span = dense_ok ? lead0 + (prev_end - first_off) / kBlk : 0;
+        // layout: forced (s3dg_set_batch_tile) or least cost
+        uint32_t tshift = kTileShiftMax;
+        if (c->tile_shift == 0 && c->tile_force_dense && dense_ok) tshift = 0;
+        else if (c->tile_shift) tshift = c->tile_shift;
+        else {
+            double best = 1e300;
+            for (uint32_t sh = kTileShiftMax; sh >= kTileShiftMin; --sh) {
+                const double cost = kDeadSlotCost * (double)((ntiles[sh] << sh) - blocks) + kRecordCost * ntiles[sh];
+                if (cost < best) { best = cost; tshift = sh; }
+            }
+            if (dense_ok && kDeadSlotCost * (double)(span - blocks) + kRecordCost * (double)span < best) tshift = 0;
+        }
+        // staging: host buffer free once its last upload finished, device copy
+        // once the k_batch_map that read it finished
+        StreamState::Stage &G = S->stage[S->next];
+        S->next ^= 1;
+        HIP_TRY(hipEventSynchronize(G.uploaded), "hipEventSynchronize(batch staging)");
+        if (m > G.cap) {
+            HIP_TRY(hipEventSynchronize(G.consumed), "hipEventSynchronize(batch staging)");
+            if (G.host) (void)hipHostFree(G.host);
+            if (G.dev) (void)hipFree(G.dev);
+            G.host = nullptr; G.dev = nullptr; G.cap = 0;
+            const uint64_t cap = m < 1024 ? 1024 : m;
+            HIP_TRY(hipHostMalloc((void **)&G.host, cap * sizeof(BatchEnt), hipHostMallocDefault),
+                    "hipHostMalloc(batch staging)");
+            HIP_TRY(hipMalloc((void **)&G.dev, cap * sizeof(BatchEnt)), "hipMalloc(batch staging)");
+            G.cap = cap;
+        }
+        // pass 2: the entries and their record ranges
+        uint64_t rec = 0, j = 0;
+        for (uint64_t k = k0; k < k1; ++k) {
+            const s3dg_obj_desc &o = d[k];
+            if (o.size == 0) continue;
+            const uint64_t nb = (o.size + kBlk - 1) / kBlk;
+            BatchEnt &e = G.host[j];
+            e.dst_off = o.dst_off;
+            e.size = o.size;
+            e.entropy = o.entropy;
+            e.dedup = o.dedup;
+            e.f_num = o.f_num;
+            e.f_den = o.f_den;
+            if (tshift == 0) {
+                const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
+                e.blk0 = g0;
+                e.rec_lo = j == 0 ? 0 : g0;
+                if (j > 0) G.host[j - 1].rec_hi = g0;   // the gap before this object: dead records
+                e.rec_hi = g0 + nb;
+            } else {
+                const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
+                e.rec_lo = rec;
+                rec += (nb + lead + (1ull << tshift) - 1) >> tshift;
+                e.rec_hi = rec;
+                e.blk0 = (e.rec_lo << tshift) + lead;
+            }
+            ++j;
+        }
+        const uint64_t recs = tshift == 0 ? span : rec;
+        if (int r = tiles_reserve(S, recs, s)) return r;
+        HIP_TRY(hipStreamWaitEvent(S->up, G.consumed, 0), "hipStreamWaitEvent");
+        HIP_TRY(hipMemcpyAsync(G.dev, G.host, m * sizeof(BatchEnt), hipMemcpyHostToDevice, S->up),
+                "hipMemcpyAsync(batch entries)");
+        HIP_TRY(hipEventRecord(G.uploaded, S->up), "hipEventRecord");
+        HIP_TRY(hipStreamWaitEvent(s, G.uploaded, 0), "hipStreamWaitEvent");
+        HIP_TRY(launch_batch_map(G.dev, m, S->tiles, tshift, s), "launch k_batch_map");
+        HIP_TRY(hipEventRecord(G.consumed, s), "hipEventRecord");
+        HIP_TRY(launch_batch_tiles(lc, (uint8_t *)dst_base, recs, tshift, S->tiles, c->base_dev, s),
+                "launch k_fill_batch");
+        k0 = k1;
+    }
     return S3DG_OK;
 }
 
@@ -706,11 +817,37 @@ int s3dg_write_ceiling_tiled(s3dg_ctx *c, void *dst, uint64_t len, uint32_t patt
     if (len == 0) return S3DG_OK;
     hipStream_t s = (hipStream_t)stream;
     const uint64_t nthr = (len / kBlk + 63) / 64;
-    std::lock_guard<std::mutex> g(c->mu);
-    if (int r = tile_map_acquire(c, nthr, s)) return r;
-    HIP_TRY(launch_write_ceiling(cfg_for(c, true), (uint8_t *)dst, len, pattern, c->tile_obj, nthr, s),
+    StreamState *S = stream_state(c, s);
+    std::lock_guard<std::mutex> g(S->mu);
+    if (int r = tiles_reserve(S, nthr, s)) return r;
+    HIP_TRY(launch_write_ceiling(cfg_for(c, true), (uint8_t *)dst, len, pattern, S->tiles, nthr, s),
             "launch k_write_ceiling(tiled)");
-    HIP_TRY(hipEventRecord(c->tile_free, s), "hipEventRecord");
+    return S3DG_OK;
+}
+
+int s3dg_write_ceiling_fill(s3dg_ctx *c, void *dst, uint64_t len, void *stream) {
+    CTX_SCOPE(c);
+    if (!dst || !aligned16(dst) || (len % kBlk))
+        return fail(S3DG_EINVAL, "dst must be 16-byte aligned and len a multiple of 4096");
+    if (len == 0) return S3DG_OK;
+    hipStream_t s = (hipStream_t)stream;
+    // the tiled fill's launch for len bytes as 8 MiB objects (d1 c1 prefix
+    // parameters; one object when len < 8 MiB)
+    constexpr uint64_t kObj = 8ull << 20;
+    if (len > kObj && len % kObj) return fail(S3DG_EINVAL, "len must be < 8 MiB or a multiple of 8 MiB");
+    const uint64_t n_objs = (len + kObj - 1) / kObj;
+    const uint64_t obj = len < kObj ? len : kObj;
+    PrefixParams pp;
+    if (int r = make_prefix(obj / kBlk, 1, 0, 1, &pp)) return r;
+    const uint32_t lead = (uint32_t)(((uintptr_t)dst >> 12) & 7);
+    const uint32_t tshift = kTileShiftMax;
+    const uint64_t tpo = (obj / kBlk + lead + (1ull << tshift) - 1) >> tshift;
+    StreamState *S = stream_state(c, s);
+    std::lock_guard<std::mutex> g(S->mu);
+    if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
+    HIP_TRY(launch_fill_uniform_tiles_ablated(cfg_for(c, true), (uint8_t *)dst, obj, kObj, n_objs, (uint32_t)tpo,
+                                              tshift, lead, pp, S->tiles, c->base_dev, s),
+            "launch k_fill_batch(ablated)");
     return S3DG_OK;
 }
 
@@ -776,170 +913,4 @@ int s3dg_sync(s3dg_ctx *c, void *stream) {
 
 }  // extern "C"
 
-// ---- host-buffer drop-ins ----------------------------------------------------
-
-namespace {
-
-struct DefaultCtx {
-    std::mutex mu;
-    s3dg_ctx *ctx = nullptr;
-    // base blocks in HBM, each uploaded once: A_BASE_BLOCK (random, once per
-    // process, src/constants.rs:715-720), BASE_BLOCK (:725-729), and the
-    // caller's block of a seeded call (re-uploaded per call; calls are
-    // serialised by `mu` and each drains its streams before returning)
-    void *base_proc = nullptr, *base_proc2 = nullptr, *base_user = nullptr;
-    void *scratch[2] = {nullptr, nullptr};
-    hipStream_t st[2] = {nullptr, nullptr};
-    static constexpr uint64_t kChunk = 64ull << 20;   // 64 MiB per device chunk
-};
-
-DefaultCtx &dflt() {
-    static DefaultCtx *d = new DefaultCtx();   // intentionally leaked: outlives atexit
-    return *d;
-}
-
-int random_bytes(uint8_t *dst, size_t n);
-
-int dflt_init(DefaultCtx &D) {
-    if (D.ctx) return S3DG_OK;
-    int dev = 0;
-    if (const char *e = getenv("S3DLIO_GPU_DEVICE")) dev = atoi(e);
-    s3dg_ctx *c = nullptr;
-    if (int r = s3dg_ctx_create(dev, &c)) return r;
-    for (int k = 0; k < 2; ++k) {
-        HIP_TRY(hipMalloc(&D.scratch[k], DefaultCtx::kChunk), "hipMalloc(scratch)");
-        HIP_TRY(hipStreamCreateWithFlags(&D.st[k], hipStreamNonBlocking), "hipStreamCreate");
-    }
-    uint8_t b[kBlk];
-    HIP_TRY(hipMalloc(&D.base_user, kBlk), "hipMalloc(base block)");
-    HIP_TRY(hipMalloc(&D.base_proc, kBlk), "hipMalloc(base block)");
-    if (int r = random_bytes(b, kBlk)) return r;
-    HIP_TRY(hipMemcpy(D.base_proc, b, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
-    HIP_TRY(hipMalloc(&D.base_proc2, kBlk), "hipMalloc(base block)");
-    if (int r = random_bytes(b, kBlk)) return r;
-    HIP_TRY(hipMemcpy(D.base_proc2, b, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
-    D.ctx = c;
-    return S3DG_OK;
-}
-
-// Generate into a host buffer through two 64 MiB device chunks on two
-// streams, so chunk k+1's kernel overlaps chunk k's D2H copy.  `pp` selects
-// the layout (controlled, or f_den = 0: generate_random_data's); `base` is
-// the device base block.
-int fill_host(DefaultCtx &D, uint8_t *buf, uint64_t len, const PrefixParams &pp, uint64_t entropy,
-              const void *base) {
-    CTX_SCOPE(D.ctx);     // the calling thread may have another device current
-    const uint64_t nb = (len + kBlk - 1) / kBlk;
-    const uint64_t cb = DefaultCtx::kChunk / kBlk;
-    for (uint64_t b0 = 0, k = 0; b0 < nb; b0 += cb, ++k) {
-        const uint64_t b1 = b0 + cb < nb ? b0 + cb : nb;
-        const int sl = (int)(k & 1);
-        HIP_TRY(launch_fill_stream(cfg_for(D.ctx), (uint8_t *)D.scratch[sl], len, 0, 1, (uint32_t)b0,
-                                   (uint32_t)b1, entropy, 0, pp, base, D.st[sl]),
-                "launch k_fill_stream(host chunk)");
-        const uint64_t off = b0 * kBlk;
-        const uint64_t n = (b1 * kBlk < len ? b1 * kBlk : len) - off;
-        HIP_TRY(hipMemcpyAsync(buf + off, D.scratch[sl], n, hipMemcpyDeviceToHost, D.st[sl]),
-                "hipMemcpyAsync(D2H)");
-    }
-    HIP_TRY(hipStreamSynchronize(D.st[0]), "hipStreamSynchronize");
-    HIP_TRY(hipStreamSynchronize(D.st[1]), "hipStreamSynchronize");
-    return S3DG_OK;
-}
-
-int fill_host_controlled(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t dedup, uint64_t compress,
-                         uint64_t entropy, const void *base) {
-    uint32_t fn, fd;
-    if (int r = s3dg_compress_ratio(compress, &fn, &fd)) return r;
-    const uint64_t nb = (len + kBlk - 1) / kBlk;
-    PrefixParams pp;
-    if (int r = make_prefix(nb, dedup, fn, fd, &pp)) return r;
-    return fill_host(D, buf, len, pp, entropy, base);
-}
-
-// generate_random_data layout (seeded analogue) into a host buffer; block i
-// seeded entropy + i.
-int fill_host_random(DefaultCtx &D, uint8_t *buf, uint64_t len, uint64_t entropy, const void *base) {
-    const uint64_t nb = (len + kBlk - 1) / kBlk;
-    if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
-    PrefixParams pp{};
-    pp.unique = 0xFFFFFFFFu;
-    pp.f_den = 0;
-    pp.m_unique = fastmod_magic(1);
-    pp.m_fden = fastmod_magic(1);
-    return fill_host(D, buf, len, pp, entropy, base);
-}
-
-int random_bytes(uint8_t *dst, size_t n) {
-    size_t got = 0;
-    while (got < n) {
-        ssize_t k = getrandom(dst + got, n - got, 0);
-        if (k <= 0) return fail(S3DG_EINVAL, "getrandom failed");
-        got += (size_t)k;
-    }
-    return S3DG_OK;
-}
-
-uint64_t time_entropy() {      // SystemTime::now() ... as_nanos() as u64, :192-195
-    timespec ts;
-    clock_gettime(CLOCK_REALTIME, &ts);
-    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-}
-
-}  // namespace
-
-extern "C" {
-
-int s3dg_internal_fail(int code, const char *msg) { return fail(code, msg); }
-
-s3dg_ctx *s3dg_internal_default_ctx(int *err) {
-    DefaultCtx &D = dflt();
-    std::lock_guard<std::mutex> g(D.mu);
-    const int r = dflt_init(D);
-    if (err) *err = r;
-    return r ? nullptr : D.ctx;
-}
-
-// generate_random_data payload for generate_object: seeded (ctx default base
-// block, entropy = seed) or unseeded (time entropy + per-process BASE_BLOCK).
-int s3dg_internal_random_host(uint8_t *buf, uint64_t len, uint64_t entropy, int use_process_base) {
-    if (len == 0) return S3DG_OK;
-    DefaultCtx &D = dflt();
-    std::lock_guard<std::mutex> g(D.mu);
-    if (int r = dflt_init(D)) return r;
-    if (!use_process_base) return fill_host_random(D, buf, len, entropy, D.ctx->base_dev);
-    return fill_host_random(D, buf, len, time_entropy(), D.base_proc2);
-}
-
-int s3dlio_generate_random_data(uint8_t *buf, size_t size) {
-    if (size == 0) return S3DG_OK;
-    if (!buf) return fail(S3DG_EINVAL, "null buffer");
-    return s3dg_internal_random_host(buf, size, 0, 1);
-}
-
-int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress) {
-    if (len == 0) return S3DG_OK;
-    if (!buf) return fail(S3DG_EINVAL, "null buffer");
-    DefaultCtx &D = dflt();
-    std::lock_guard<std::mutex> g(D.mu);
-    if (int r = dflt_init(D)) return r;
-    return fill_host_controlled(D, buf, len, dedup, compress, time_entropy(), D.base_proc);
-}
-
-int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, size_t compress,
-                                       uint64_t entropy, const uint8_t *base4096) {
-    if (len == 0) return S3DG_OK;
-    if (!buf) return fail(S3DG_EINVAL, "null buffer");
-    DefaultCtx &D = dflt();
-    std::lock_guard<std::mutex> g(D.mu);
-    if (int r = dflt_init(D)) return r;
-    const void *base = D.ctx->base_dev;
-    if (base4096) {
-        CTX_SCOPE(D.ctx);
-        HIP_TRY(hipMemcpy(D.base_user, base4096, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
-        base = D.base_user;
-    }
-    return fill_host_controlled(D, buf, len, dedup, compress, entropy, base);
-}
-
-}  // extern "C"
+extern "C" int s3dg_internal_fail(int code, const char *msg) { return fail(code, msg); }

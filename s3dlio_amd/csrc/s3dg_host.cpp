@@ -1,0 +1,434 @@
+// s3dg_host.cpp — host-buffer drop-ins on every visible GPU.
+//
+// The reference's host-memory entry points (fill_controlled_data,
+// src/data_gen.rs:151; generate_random_data, :102; the dgen-backed
+// DataGenerator / Generator / generate_data, src/data_gen.rs:253-371,
+// src/python_api/python_datagen_api.rs:49-365) are synchronous, thread-safe
+// and run in parallel from many threads (tests/test_s3dlio_datagen.py:174-204
+// runs 8 generators at once).  Here they run on a pool of SLOTS, one per GPU
+// by default:
+//   * a slot = one device, its context (default base block), its copies of the
+//     per-process random base blocks (A_BASE_BLOCK / BASE_BLOCK,
+//     src/constants.rs:715-729) and a pool of staging sets (two 64 MiB device
+//     chunks + two streams + a 4 KiB block for a caller's base block);
+//   * every call takes a slot round-robin and a staging set of its own, so
+//     concurrent calls never wait on a lock while the GPU works, and calls on
+//     different slots use different GPUs (and PCIe links);
+//   * a large call (>= 2 x kSplitMin bytes) is cut into contiguous block ranges,
+//     one per slot, generated in parallel (one host thread per extra slot).
+// Slot devices: S3DLIO_GPU_DEVICE=k pins every call to GPU k;
+// S3DLIO_GPU_DEVICES=a,b,... lists them (repeats give several slots on one
+// GPU); neither set: every visible GPU.  Bytes never depend on the slot.
+#include "s3dg_internal.h"
+#include "s3dlio_gpu.h"
+
+#include <sys/random.h>
+#include <time.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+using namespace s3dg;
+
+namespace {
+
+constexpr uint64_t kChunk = 64ull << 20;       // bytes per device staging chunk
+constexpr uint64_t kSplitMin = 128ull << 20;   // smallest per-slot share of a split call
+constexpr int kMaxSlots = 64;
+
+#define H_TRY(expr, what)                                                                  \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return s3dg_internal_fail(S3DG_EHIP, (std::string(what) + ": " + hipGetErrorString(e_)).c_str()); \
+    } while (0)
+
+struct Slot {
+    int device = 0;
+    std::mutex mu;                      // init and the idle list
+    s3dg_ctx *ctx = nullptr;            // set last: non-null = initialised
+    void *base_proc[2] = {nullptr, nullptr};   // A_BASE_BLOCK, BASE_BLOCK copies in HBM
+    std::vector<HostStaging *> idle;
+};
+
+struct Pool {
+    std::mutex mu;
+    bool ready = false;
+    std::vector<Slot *> slots;          // never freed: outlives HIP teardown
+    uint8_t proc_base[2][kBlk];         // per-process random blocks (same on every slot)
+    std::atomic<uint64_t> ticket{0};
+};
+
+Pool &pool() {
+    static Pool *p = new Pool();
+    return *p;
+}
+
+int random_bytes(uint8_t *dst, size_t n) {
+    size_t got = 0;
+    while (got < n) {
+        ssize_t k = getrandom(dst + got, n - got, 0);
+        if (k <= 0) return s3dg_internal_fail(S3DG_EINVAL, "getrandom failed");
+        got += (size_t)k;
+    }
+    return S3DG_OK;
+}
+
+uint64_t time_entropy() {      // SystemTime::now() ... as_nanos() as u64, src/data_gen.rs:192-195
+    timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+int pool_init(Pool &P) {
+    std::lock_guard<std::mutex> g(P.mu);
+    if (P.ready) return S3DG_OK;
+    int ndev = 0;
+    H_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (ndev <= 0) return s3dg_internal_fail(S3DG_EHIP, "no GPU visible");
+    int devs[kMaxSlots], n = 0;
+    if (int r = s3dg_host_parse_devices(getenv("S3DLIO_GPU_DEVICE"), getenv("S3DLIO_GPU_DEVICES"), ndev, devs,
+                                        kMaxSlots, &n))
+        return r;
+    for (int k = 0; k < 2; ++k)
+        if (int r = random_bytes(P.proc_base[k], kBlk)) return r;
+    for (int k = 0; k < n; ++k) {
+        Slot *s = new Slot();
+        s->device = devs[k];
+        P.slots.push_back(s);
+    }
+    P.ready = true;
+    return S3DG_OK;
+}
+
+// Context and base blocks of a slot, created under the slot's device; on any
+// failure everything allocated so far is released and the slot stays
+// uninitialised (the next call retries).
+int slot_init(Pool &P, Slot *S) {
+    std::lock_guard<std::mutex> g(S->mu);
+    if (S->ctx) return S3DG_OK;
+    s3dg_ctx *c = nullptr;
+    if (int r = s3dg_ctx_create(S->device, &c)) return r;
+    DeviceScope ds(S->device);
+    void *b[2] = {nullptr, nullptr};
+    hipError_t e = ds.err;
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+        e = hipMalloc(&b[k], kBlk);
+        if (e == hipSuccess) e = hipMemcpy(b[k], P.proc_base[k], kBlk, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        for (void *p : b)
+            if (p) (void)hipFree(p);
+        s3dg_ctx_destroy(c);
+        return s3dg_internal_fail(S3DG_EHIP, (std::string("host slot init: ") + hipGetErrorString(e)).c_str());
+    }
+    S->base_proc[0] = b[0];
+    S->base_proc[1] = b[1];
+    S->ctx = c;
+    return S3DG_OK;
+}
+
+int get_slot(int k, Slot **out) {
+    Pool &P = pool();
+    if (int r = pool_init(P)) return r;
+    if (k < 0 || k >= (int)P.slots.size()) return s3dg_internal_fail(S3DG_EINVAL, "host slot out of range");
+    if (int r = slot_init(P, P.slots[k])) return r;
+    *out = P.slots[k];
+    return S3DG_OK;
+}
+
+void staging_free(HostStaging *sg) {
+    for (int q = 0; q < 2; ++q) {
+        if (sg->buf[q]) (void)hipFree(sg->buf[q]);
+        if (sg->st[q]) (void)hipStreamDestroy(sg->st[q]);
+    }
+    if (sg->base_user) (void)hipFree(sg->base_user);
+    delete sg;
+}
+
+const void *base_for(Slot *S, HostStaging *sg, const HostJob &J) {
+    switch (J.base) {
+    case HostJob::kBaseProcA: return S->base_proc[0];
+    case HostJob::kBaseProcB: return S->base_proc[1];
+    case HostJob::kBaseUser: return sg->base_user;
+    default: return ctx_base(S->ctx);
+    }
+}
+
+}  // namespace
+
+namespace s3dg {
+
+int host_slot_count(int *n) {
+    Pool &P = pool();
+    if (int r = pool_init(P)) return r;
+    *n = (int)P.slots.size();
+    return S3DG_OK;
+}
+
+int host_next_slot(int *slot) {
+    int n = 0;
+    if (int r = host_slot_count(&n)) return r;
+    *slot = (int)(pool().ticket.fetch_add(1) % (uint64_t)n);
+    return S3DG_OK;
+}
+
+int host_staging_acquire(int slot, HostStaging **out) {
+    Slot *S = nullptr;
+    if (int r = get_slot(slot, &S)) return r;
+    {
+        std::lock_guard<std::mutex> g(S->mu);
+        if (!S->idle.empty()) {
+            *out = S->idle.back();
+            S->idle.pop_back();
+            return S3DG_OK;
+        }
+    }
+    DeviceScope ds(S->device);
+    HostStaging *sg = new HostStaging();
+    sg->slot = slot;
+    hipError_t e = ds.err;
+    for (int q = 0; q < 2 && e == hipSuccess; ++q) {
+        e = hipMalloc(&sg->buf[q], kChunk);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&sg->st[q], hipStreamNonBlocking);
+    }
+    if (e == hipSuccess) e = hipMalloc(&sg->base_user, kBlk);
+    if (e != hipSuccess) {
+        staging_free(sg);
+        return s3dg_internal_fail(S3DG_EHIP, (std::string("host staging: ") + hipGetErrorString(e)).c_str());
+    }
+    *out = sg;
+    return S3DG_OK;
+}
+
+void host_staging_release(HostStaging *sg) {
+    if (!sg) return;
+    Slot *S = pool().slots[sg->slot];
+    {
+        DeviceScope ds(S->device);
+        for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);
+    }
+    std::lock_guard<std::mutex> g(S->mu);
+    S->idle.push_back(sg);
+}
+
+// Bytes [pos, pos+n) of the job's object into host `buf` on the staging set's
+// slot: the covering generation blocks go through the two device chunks on
+// two streams (chunk k+1's kernel overlaps chunk k's D2H), then exactly the
+// requested bytes are copied out.
+int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
+    if (n == 0) return S3DG_OK;
+    Slot *S = pool().slots[sg->slot];
+    DeviceScope ds(S->device);
+    H_TRY(ds.err, "hipSetDevice");
+    if (J.base == HostJob::kBaseUser)
+        H_TRY(hipMemcpy(sg->base_user, J.user_base, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
+    const void *base = base_for(S, sg, J);
+    const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
+    const uint64_t per = kChunk / unit;
+    const uint64_t b0 = pos / unit, b1 = (pos + n + unit - 1) / unit;
+    int k = 0;
+    for (uint64_t pb = b0; pb < b1; pb += per, ++k) {
+        const uint64_t pe = pb + per < b1 ? pb + per : b1;
+        const int sl = k & 1;
+        if (J.dgen) {
+            if (int r = s3dg_dgen_fill(S->ctx, sg->buf[sl], J.obj_len, pb, pe, J.dedup, J.f_num, J.f_den, J.entropy,
+                                       sg->st[sl]))
+                return r;
+        } else {
+            H_TRY(launch_fill_stream(ctx_stream_cfg(S->ctx), (uint8_t *)sg->buf[sl], J.obj_len, 0, 1, (uint32_t)pb,
+                                     (uint32_t)pe, J.entropy, 0, J.pp, base, sg->st[sl]),
+                  "launch k_fill_stream(host chunk)");
+        }
+        const uint64_t lo = pb * unit > pos ? pb * unit : pos;
+        const uint64_t hi = pe * unit < pos + n ? pe * unit : pos + n;
+        H_TRY(hipMemcpyAsync(buf + (lo - pos), (uint8_t *)sg->buf[sl] + (lo - pb * unit), hi - lo,
+                             hipMemcpyDeviceToHost, sg->st[sl]),
+              "hipMemcpyAsync(D2H)");
+    }
+    H_TRY(hipStreamSynchronize(sg->st[0]), "hipStreamSynchronize");
+    H_TRY(hipStreamSynchronize(sg->st[1]), "hipStreamSynchronize");
+    return S3DG_OK;
+}
+
+// The same, cut into one contiguous range per slot when the request is large
+// enough: part 0 runs on `sg0` (the caller's staging, on slot sg0->slot) in
+// the calling thread, part p on slot (sg0->slot + p) mod slots in a thread of
+// its own with a staging set of its own.
+int host_run_split(HostStaging *sg0, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
+    int nslots = 1;
+    if (int r = host_slot_count(&nslots)) return r;
+    const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
+    uint64_t parts = n / kSplitMin;
+    if (parts > (uint64_t)nslots) parts = (uint64_t)nslots;
+    if (parts < 2) return host_run(sg0, J, buf, pos, n);
+    // part boundaries on generation-block edges
+    std::vector<uint64_t> cut(parts + 1);
+    cut[0] = pos;
+    cut[parts] = pos + n;
+    for (uint64_t p = 1; p < parts; ++p) {
+        uint64_t c = pos + n / parts * p;
+        c = c / unit * unit;
+        cut[p] = c < cut[p - 1] ? cut[p - 1] : c;
+    }
+    std::vector<int> rc(parts, S3DG_OK);
+    std::vector<std::string> err(parts);
+    std::vector<std::thread> th;
+    for (uint64_t p = 1; p < parts; ++p) {
+        th.emplace_back([&, p]() {
+            HostStaging *sg = nullptr;
+            int r = host_staging_acquire((int)((sg0->slot + p) % (uint64_t)nslots), &sg);
+            if (r == S3DG_OK) r = host_run(sg, J, buf + (cut[p] - pos), cut[p], cut[p + 1] - cut[p]);
+            if (r != S3DG_OK) err[p] = s3dg_last_error();
+            host_staging_release(sg);
+            rc[p] = r;
+        });
+    }
+    rc[0] = host_run(sg0, J, buf, cut[0], cut[1] - cut[0]);
+    for (auto &t : th) t.join();
+    for (uint64_t p = 1; p < parts; ++p)
+        if (rc[p] != S3DG_OK && rc[0] == S3DG_OK) return s3dg_internal_fail(rc[p], err[p].c_str());
+    return rc[0];
+}
+
+// One-shot: a slot round-robin, a staging set for the call, split over slots.
+static int host_oneshot(const HostJob &J, uint8_t *buf, uint64_t len) {
+    int slot = 0;
+    if (int r = host_next_slot(&slot)) return r;
+    HostStaging *sg = nullptr;
+    if (int r = host_staging_acquire(slot, &sg)) return r;
+    const int r = host_run_split(sg, J, buf, 0, len);
+    host_staging_release(sg);
+    return r;
+}
+
+static int controlled_job(HostJob &J, uint64_t len, uint64_t dedup, uint64_t compress) {
+    uint32_t fn, fd;
+    if (int r = s3dg_compress_ratio(compress, &fn, &fd)) return r;
+    J.obj_len = len;
+    return make_prefix((len + kBlk - 1) / kBlk, dedup, fn, fd, &J.pp);
+}
+
+}  // namespace s3dg
+
+extern "C" {
+
+int s3dg_host_parse_devices(const char *pin, const char *list, int ndev, int *out, int cap, int *n) {
+    if (!out || !n || cap <= 0) return s3dg_internal_fail(S3DG_EINVAL, "null output");
+    *n = 0;
+    auto parse_int = [&](const char *&p, int *v) -> bool {
+        while (*p == ' ') ++p;
+        if (*p < '0' || *p > '9') return false;
+        long x = 0;
+        while (*p >= '0' && *p <= '9') {
+            x = x * 10 + (*p++ - '0');
+            if (x > 1000000) return false;
+        }
+        while (*p == ' ') ++p;
+        *v = (int)x;
+        return true;
+    };
+    if (pin && *pin) {
+        const char *p = pin;
+        int d = 0;
+        if (!parse_int(p, &d) || *p) return s3dg_internal_fail(S3DG_EINVAL, "S3DLIO_GPU_DEVICE must be a device index");
+        if (d >= ndev) return s3dg_internal_fail(S3DG_EINVAL, "S3DLIO_GPU_DEVICE out of range");
+        out[0] = d;
+        *n = 1;
+        return S3DG_OK;
+    }
+    if (list && *list) {
+        const char *p = list;
+        int k = 0;
+        for (;;) {
+            int d = 0;
+            if (!parse_int(p, &d)) return s3dg_internal_fail(S3DG_EINVAL, "S3DLIO_GPU_DEVICES must be a comma list of device indices");
+            if (d >= ndev) return s3dg_internal_fail(S3DG_EINVAL, "S3DLIO_GPU_DEVICES names a device out of range");
+            if (k >= cap) return s3dg_internal_fail(S3DG_EINVAL, "S3DLIO_GPU_DEVICES lists too many slots");
+            out[k++] = d;
+            if (!*p) break;
+            if (*p++ != ',') return s3dg_internal_fail(S3DG_EINVAL, "S3DLIO_GPU_DEVICES must be a comma list of device indices");
+        }
+        *n = k;
+        return S3DG_OK;
+    }
+    if (ndev <= 0) return s3dg_internal_fail(S3DG_EINVAL, "no GPU visible");
+    for (int d = 0; d < ndev && d < cap; ++d) out[(*n)++] = d;
+    return S3DG_OK;
+}
+
+int s3dg_host_slot_count(int *out) {
+    if (!out) return s3dg_internal_fail(S3DG_EINVAL, "null output");
+    return host_slot_count(out);
+}
+
+int s3dg_host_slot_device(int slot, int *device) {
+    if (!device) return s3dg_internal_fail(S3DG_EINVAL, "null output");
+    Pool &P = pool();
+    if (int r = pool_init(P)) return r;
+    if (slot < 0 || slot >= (int)P.slots.size()) return s3dg_internal_fail(S3DG_EINVAL, "host slot out of range");
+    *device = P.slots[slot]->device;
+    return S3DG_OK;
+}
+
+int s3dg_host_slot_context(int slot, s3dg_ctx **out) {
+    if (!out) return s3dg_internal_fail(S3DG_EINVAL, "null output");
+    *out = nullptr;
+    if (slot < 0) {
+        if (int r = host_next_slot(&slot)) return r;
+    }
+    Slot *S = nullptr;
+    if (int r = get_slot(slot, &S)) return r;
+    *out = S->ctx;
+    return S3DG_OK;
+}
+
+// generate_random_data payload for generate_object: seeded (the slot
+// context's default base block, entropy = seed) or unseeded (time entropy +
+// the per-process BASE_BLOCK).
+int s3dg_internal_random_host(uint8_t *buf, uint64_t len, uint64_t entropy, int use_process_base) {
+    if (len == 0) return S3DG_OK;
+    const uint64_t nb = (len + kBlk - 1) / kBlk;
+    if (nb > 0xFFFFFFFFull) return s3dg_internal_fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    HostJob J;
+    J.obj_len = len;
+    J.pp = random_layout_prefix();
+    J.entropy = use_process_base ? time_entropy() : entropy;
+    J.base = use_process_base ? HostJob::kBaseProcB : HostJob::kBaseCtx;
+    return host_oneshot(J, buf, len);
+}
+
+int s3dlio_generate_random_data(uint8_t *buf, size_t size) {
+    if (size == 0) return S3DG_OK;
+    if (!buf) return s3dg_internal_fail(S3DG_EINVAL, "null buffer");
+    return s3dg_internal_random_host(buf, size, 0, 1);
+}
+
+int s3dlio_fill_controlled_data(uint8_t *buf, size_t len, size_t dedup, size_t compress) {
+    if (len == 0) return S3DG_OK;                                    // :154-156
+    if (!buf) return s3dg_internal_fail(S3DG_EINVAL, "null buffer");
+    HostJob J;
+    if (int r = controlled_job(J, len, dedup, compress)) return r;
+    J.entropy = time_entropy();
+    J.base = HostJob::kBaseProcA;
+    return host_oneshot(J, buf, len);
+}
+
+int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup, size_t compress,
+                                       uint64_t entropy, const uint8_t *base4096) {
+    if (len == 0) return S3DG_OK;
+    if (!buf) return s3dg_internal_fail(S3DG_EINVAL, "null buffer");
+    HostJob J;
+    if (int r = controlled_job(J, len, dedup, compress)) return r;
+    J.entropy = entropy;
+    J.base = base4096 ? HostJob::kBaseUser : HostJob::kBaseCtx;
+    J.user_base = base4096;
+    return host_oneshot(J, buf, len);
+}
+
+}  // extern "C"

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 extern "C" int s3dg_internal_fail(int code, const char *msg);
+struct s3dg_ctx;
 
 namespace s3dg {
 
@@ -15,6 +16,8 @@ constexpr uint64_t kDgenBlock = 1ull << 20;   // DGEN_BLOCK_SIZE src/constants.r
 // batch tiles (tile -> object map granule) are 2^tshift blocks, tshift in
 // [kTileShiftMin, kTileShiftMax], chosen per launch (s3dg_capi.cpp pick_tile_shift)
 constexpr uint32_t kTileShiftMin = 3, kTileShiftMax = 6;
+// tshift 0 (one record per 4 KiB granule of the batch's address range, no
+// per-object lead) is the dense layout for small packed objects
 constexpr int kWavesPerWG = 4;
 
 // Zero-prefix parameters of one object: const_len(u) =
@@ -33,18 +36,23 @@ struct PrefixParams {
 // Kurz 2019, "Faster remainder by direct computation"); exact for all a, d < 2^32.
 inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
 
-// Device-side table entry of a mixed-size batch (64 B).
-struct ObjEntry {
+// Batch entry as uploaded (64 B): the caller's descriptor plus its record
+// range.  Records [rec_lo, rec_hi) of the launch belong to this object; its
+// block 0 sits at slot blk0 (slot = record << tshift + position in the tile).
+// k_batch_map derives the prefix parameters on the device.
+struct BatchEnt {
     uint64_t dst_off;
     uint64_t size;
     uint64_t entropy;
-    uint64_t tile_begin;   // exclusive prefix sum of tiles per object
-    PrefixParams pp;
-    uint32_t lead;         // dead slots before block 0 in the first tile (XCD alignment)
-    uint32_t pad;
+    uint64_t dedup;
+    uint64_t rec_lo, rec_hi;
+    uint64_t blk0;
+    uint32_t f_num, f_den;
 };
+static_assert(sizeof(BatchEnt) == 64, "BatchEnt is 64 bytes");
 
-// One 64-block tile of a batch object, written by k_tile_map so the fill
+// One tile (2^tshift slots) of a batch object, written by k_batch_map /
+// k_tile_map_uniform so the fill
 // kernel reaches everything with a single 64-byte scalar load.
 struct TileRec {
     uint64_t dst_off;      // byte offset of the object
@@ -77,9 +85,12 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               uint32_t blk_hi, uint64_t seed_base, uint64_t first_obj,
                               PrefixParams pp, const void *base_dev, hipStream_t s);
 
-hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, uint32_t tshift, TileRec *tiles,
-                             const void *base_dev, hipStream_t s);
+// Batch records built on the device from uploaded BatchEnts (k_batch_map:
+// prefix parameters per object, then its records), then k_fill_batch over
+// total_recs << tshift slots.
+hipError_t launch_batch_map(const BatchEnt *ents, uint64_t n, TileRec *tiles, uint32_t tshift, hipStream_t s);
+hipError_t launch_batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t total_tiles, uint32_t tshift,
+                              TileRec *tiles, const void *base_dev, hipStream_t s);
 
 // A uniform stream through the batch kernel: records built on the device
 // (k_tile_map_uniform), then k_fill_batch.
@@ -87,6 +98,11 @@ hipError_t launch_fill_uniform_tiles(const LaunchCfg &lc, uint8_t *dst, uint64_t
                                      uint64_t n_objs, uint32_t tiles_per_obj, uint32_t tshift, uint32_t lead,
                                      uint64_t ent0, PrefixParams pp, TileRec *tiles, const void *base_dev,
                                      hipStream_t s);
+
+// The store-only reference of the same launch (s3dg_write_ceiling_fill).
+hipError_t launch_fill_uniform_tiles_ablated(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size, uint64_t stride,
+                                             uint64_t n_objs, uint32_t tiles_per_obj, uint32_t tshift, uint32_t lead,
+                                             PrefixParams pp, TileRec *tiles, const void *base_dev, hipStream_t s);
 
 // K2 keystream launch: chunks [chunk0, chunk0 + nchunks) of an obj_len-byte
 // object, chunk k at dst + (k - chunk0) * chunk_bytes.
@@ -122,6 +138,44 @@ hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu);
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
                                 uint32_t pattern, const TileRec *thr, uint64_t nthr, hipStream_t s);
 
+
+// ---- context internals (s3dg_capi.cpp) ---------------------------------------
+// Zero-prefix parameters of an object of nblocks 4 KiB blocks
+// (src/data_gen.rs:162-190); S3DG_EINVAL on a bad ratio.
+int make_prefix(uint64_t nblocks, uint64_t dedup, uint32_t f_num, uint32_t f_den, PrefixParams *pp);
+// generate_random_data's block layout (f_den = 0, src/data_gen.rs:102-132)
+PrefixParams random_layout_prefix();
+LaunchCfg ctx_stream_cfg(const s3dg_ctx *c);   // the context's stream-kernel launch knobs
+const void *ctx_base(const s3dg_ctx *c);       // the context's 4 KiB base block in HBM
+
+// ---- host-buffer engine (s3dg_host.cpp) --------------------------------------
+// Staging set of a host slot: two 64 MiB device chunks, two streams and a
+// 4 KiB device block for a caller's base block.
+struct HostStaging {
+    int slot = 0;
+    void *buf[2] = {nullptr, nullptr};
+    hipStream_t st[2] = {nullptr, nullptr};
+    void *base_user = nullptr;
+};
+// What to generate into host memory: the fill_controlled_data / random-data
+// layouts (4 KiB blocks, pp) or DG1 (dgen = true, 1 MiB blocks).
+struct HostJob {
+    enum Base { kBaseCtx, kBaseProcA, kBaseProcB, kBaseUser };
+    bool dgen = false;
+    uint64_t obj_len = 0;
+    uint64_t entropy = 0;          // block seeds u + entropy; DG1: the seed
+    PrefixParams pp{};
+    Base base = kBaseCtx;
+    const uint8_t *user_base = nullptr;
+    uint64_t dedup = 1;            // DG1
+    uint32_t f_num = 0, f_den = 1; // DG1
+};
+int host_slot_count(int *n);
+int host_next_slot(int *slot);     // round-robin
+int host_staging_acquire(int slot, HostStaging **out);
+void host_staging_release(HostStaging *sg);   // waits for its streams
+int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n);
+int host_run_split(HostStaging *sg0, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n);
 
 // ---- CRC-32 (s3dg_crc.hip) -------------------------------------------------
 uint32_t crc32_host_update(uint32_t crc, const uint8_t *p, uint64_t n);

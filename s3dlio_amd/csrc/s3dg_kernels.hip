@@ -129,6 +129,7 @@ struct Plan {
     uint64_t w1[4], w2w[4];
 };
 
+template <bool ABL = false>
 __device__ __forceinline__ void plan_block(Plan &P, uint32_t lane, uint32_t i, uint64_t size,
                                            uint64_t entropy, const PrefixParams &pp) {
     const uint32_t u = pp.unique == 0xFFFFFFFFu ? i : fastmod(i, pp.m_unique, pp.unique);  // :201
@@ -159,6 +160,7 @@ __device__ __forceinline__ void plan_block(Plan &P, uint32_t lane, uint32_t i, u
     // SmallRng::seed_from_u64(u + entropy) (:202-203): state word k =
     // mix64(seed + (k+1)*phi) — lanes 0..3 compute one word each.
     const uint64_t seed = (uint64_t)u + entropy;
+    if constexpr (ABL) return;
 #if S3DG_ABLATE & 2
     for (int q = 0; q < 4; ++q) { P.w1[q] = seed + q; P.w2w[q] = seed - q; }
     return;
@@ -254,7 +256,10 @@ __device__ __forceinline__ void store_image(BlockLds &S, uint32_t t, const u32x4
 }
 
 // IMG: the caller has already written the base image into S (batch kernel).
-template <int NT, int NW, bool IMG = false>
+// ABL: the store-only reference of the same kernel (write ceiling): block
+// geometry, LDS image, barrier and stores as the fill, without the PRNG chain
+// and the window patch phase; its bytes are wrong by design.
+template <int NT, int NW, bool IMG = false, bool ABL = false>
 __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, uint32_t wave,
                                           uint32_t i, uint64_t size, uint64_t entropy,
                                           const PrefixParams &pp, const u32x4 (&B)[4 / NW]) {
@@ -262,14 +267,16 @@ __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, 
     const uint32_t lane = t & 63;
     Plan P;
     if (wave == 0) {
-        plan_block(P, lane, i, size, entropy, pp);
+        plan_block<ABL>(P, lane, i, size, entropy, pp);
         if (lane == 0) { S.meta[0] = P.c; S.meta[1] = P.L; }
     }
     if constexpr (!IMG) store_image<NW>(S, t, B);
     __syncthreads();
 #if !(S3DG_ABLATE & 1)
-    if (wave == 0) patch_image(S, P, lane);
-    __syncthreads();
+    if constexpr (!ABL) {
+        if (wave == 0) patch_image(S, P, lane);
+        __syncthreads();
+    }
 #endif
 #pragma unroll
     for (int k = 0; k < SPL; ++k) write_block<NT>(bd, S, (int)(t + k * T) * 16);
@@ -308,7 +315,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 // 64*pf blocks ahead (one lane per 128-byte line of records) after their
 // stores, result unused, so they are in that XCD's L2 when its workgroups
 // start.  pf must exceed the resident workgroups / 64.
-template <int NT, int NW>
+template <int NT, int NW, bool ABL = false>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
                                                         uint32_t tshift, const u32x4 *base) {
@@ -333,37 +340,62 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     const int64_t ib = (int64_t)e.first + k - e.lead;
     uint8_t *const bdst = dst_base + e.dst_off + (uint64_t)ib * kBlk;
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
-    gen_block<NT, NW, true>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
+    gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
-    // 128-byte line (2 records) of the span's records
+    // 128-byte line (2 records) of the span's records (and the (q+64k)-th
+    // with one record per block, tshift 0: 128 lines)
     constexpr uint32_t kPfSpan = 256;
     const uint32_t span = kPfSpan > (2u << tshift) ? kPfSpan : (2u << tshift);
-    if (pf && (g & (span - 1)) < 8 && t < (span >> (tshift + 1))) {
-        const uint64_t pt = (((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift) + 2 * t;
-        const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
-        uint32_t dummy;
-        asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
+    const uint32_t lines = tshift ? span >> (tshift + 1) : span >> 1;
+    if (pf && (g & (span - 1)) < 8) {
+        for (uint32_t q = t; q < lines; q += 64 * NW) {
+            const uint64_t pt = (((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift) + 2 * q;
+            const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
+            uint32_t dummy;
+            asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
+        }
     }
 }
 
-// tiles[tile] = record of every 2^tshift-block tile of every object.
-__global__ __launch_bounds__(256) void k_tile_map(const ObjEntry *tab, uint64_t n, TileRec *tiles,
-                                                  uint32_t tshift) {
-    const uint64_t k = blockIdx.x;
+// Prefix parameters of one object on the device, as the host's make_prefix
+// (src/data_gen.rs:162-175; s3dg_unique_blocks' f64 round half away from zero).
+__device__ PrefixParams dev_make_prefix(uint64_t nb, uint64_t dedup, uint32_t f_num, uint32_t f_den) {
+    const uint64_t d = dedup == 0 ? 1 : dedup;
+    uint64_t U = nb;
+    if (d > 1) {
+        double r = round((double)nb / (double)d);
+        if (r < 1.0) r = 1.0;
+        U = (uint64_t)r;
+    }
+    PrefixParams pp;
+    const uint64_t tot = (uint64_t)f_num * kBlk;
+    pp.unique = U == nb ? 0xFFFFFFFFu : (uint32_t)U;
+    pp.floor_len = (uint32_t)(tot / f_den);
+    pp.rem = (uint32_t)(tot % f_den);
+    pp.f_den = f_den;
+    pp.m_unique = ~0ull / (pp.unique == 0xFFFFFFFFu ? 1u : pp.unique) + 1;
+    pp.m_fden = ~0ull / f_den + 1;
+    return pp;
+}
+
+// Records of a batch launch from its uploaded entries, one thread per object:
+// record q in [rec_lo, rec_hi) maps slot (q << tshift) + k to block
+// (q - rec_lo) << tshift + k - lead, lead = blk0 - (rec_lo << tshift).
+__global__ __launch_bounds__(256) void k_batch_map(const BatchEnt *ents, uint64_t n, TileRec *tiles,
+                                                   uint32_t tshift) {
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
-    const ObjEntry e = tab[k];
-    const uint64_t tb = 1ull << tshift;
-    const uint64_t nt = ((e.size + kBlk - 1) / kBlk + e.lead + tb - 1) >> tshift;
-    for (uint64_t q = threadIdx.x; q < nt; q += blockDim.x) {
-        TileRec r;
-        r.dst_off = e.dst_off;
-        r.size = e.size;
-        r.entropy = e.entropy;
-        r.first = (uint32_t)(q * tb);
-        r.lead = e.lead;
-        r.pp = e.pp;
-        tiles[e.tile_begin + q] = r;
+    const BatchEnt e = ents[k];
+    TileRec r;
+    r.dst_off = e.dst_off;
+    r.size = e.size;
+    r.entropy = e.entropy;
+    r.lead = (uint32_t)(e.blk0 - (e.rec_lo << tshift));
+    r.pp = dev_make_prefix((e.size + kBlk - 1) / kBlk, e.dedup, e.f_num, e.f_den);
+    for (uint64_t q = e.rec_lo; q < e.rec_hi; ++q) {
+        r.first = (uint32_t)((q - e.rec_lo) << tshift);
+        tiles[q] = r;
     }
 }
 
@@ -690,6 +722,12 @@ void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const Til
 }
 
 template <int NT, int NW>
+void launch_batch_abl_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
+                          uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b);
+}
+
+template <int NT, int NW>
 void launch_ceiling_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, uint64_t nch, uint64_t g0,
                         uint32_t pattern, const TileRec *thr, uint64_t nthr, uint32_t pf) {
     hipLaunchKernelGGL((k_write_ceiling<NT, NW>), g, dim3(64 * NW), lds, s, d, nch, g0, pattern, thr, nthr, pf);
@@ -769,29 +807,36 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
     return hipSuccess;
 }
 
-static hipError_t launch_batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t total_tiles,
-                                     uint32_t tshift, TileRec *tiles, const void *base_dev, hipStream_t s) {
+static hipError_t batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t total_tiles, uint32_t tshift,
+                              TileRec *tiles, const void *base_dev, hipStream_t s, bool ablated) {
     hipError_t e;
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
     const uint64_t total = total_tiles << tshift;
     for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
         const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
-        S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
-                      lc.prefetch_tiles, tshift, b);
+        if (ablated)
+            S3DG_DISPATCH(launch_batch_abl_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
+                          lc.prefetch_tiles, tshift, b);
+        else
+            S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
+                          lc.prefetch_tiles, tshift, b);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
-hipError_t launch_fill_batch(const LaunchCfg &lc, uint8_t *dst_base, const ObjEntry *tab,
-                             uint64_t n, uint64_t total_tiles, uint32_t tshift, TileRec *tiles,
-                             const void *base_dev, hipStream_t s) {
+hipError_t launch_batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t total_tiles, uint32_t tshift,
+                              TileRec *tiles, const void *base_dev, hipStream_t s) {
     (void)hipGetLastError();
-    hipLaunchKernelGGL(k_tile_map, dim3((uint32_t)n), dim3(256), 0, s, tab, n, tiles, tshift);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return launch_batch_tiles(lc, dst_base, total_tiles, tshift, tiles, base_dev, s);
+    return batch_tiles(lc, dst_base, total_tiles, tshift, tiles, base_dev, s, false);
+}
+
+hipError_t launch_batch_map(const BatchEnt *ents, uint64_t n, TileRec *tiles, uint32_t tshift, hipStream_t s) {
+    (void)hipGetLastError();
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_batch_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, ents, n, tiles, tshift);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill_uniform_tiles(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size, uint64_t stride,
@@ -804,7 +849,22 @@ hipError_t launch_fill_uniform_tiles(const LaunchCfg &lc, uint8_t *dst, uint64_t
                        total_tiles, tiles_per_obj, tshift, stride, obj_size, ent0, lead, pp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_batch_tiles(lc, dst, total_tiles, tshift, tiles, base_dev, s);
+    return batch_tiles(lc, dst, total_tiles, tshift, tiles, base_dev, s, false);
+}
+
+// The write ceiling in the tiled fill's own shape: the same records, grid,
+// LDS image, barrier, stores and trailing prefetch as a uniform stream
+// through k_fill_batch, without the PRNG chain and the window patches.
+hipError_t launch_fill_uniform_tiles_ablated(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_size, uint64_t stride,
+                                             uint64_t n_objs, uint32_t tiles_per_obj, uint32_t tshift, uint32_t lead,
+                                             PrefixParams pp, TileRec *tiles, const void *base_dev, hipStream_t s) {
+    (void)hipGetLastError();
+    const uint64_t total_tiles = n_objs * tiles_per_obj;
+    hipLaunchKernelGGL(k_tile_map_uniform, dim3((uint32_t)((total_tiles + 255) / 256)), dim3(256), 0, s, tiles,
+                       total_tiles, tiles_per_obj, tshift, stride, obj_size, 0ull, lead, pp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return batch_tiles(lc, dst, total_tiles, tshift, tiles, base_dev, s, true);
 }
 
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,

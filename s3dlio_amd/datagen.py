@@ -172,6 +172,11 @@ class Generator:
     def total_size(self) -> int:
         return int(lib.s3dg_gen_total_size(self._g.h))
 
+    @property
+    def slot(self) -> int:
+        """Host slot this generator runs on (s3dg_gen_slot; not in the reference)."""
+        return int(lib.s3dg_gen_slot(self._g.h))
+
 
 # ---- Rust streaming API (src/data_gen.rs:232-371) ---------------------------------
 

@@ -73,13 +73,15 @@ def _nbytes(x) -> int | None:
     return None
 
 
-def _stream(stream) -> int:
+def _stream(stream, device: int | None = None) -> int:
     """hipStream_t handle: an int, a torch stream, or None = torch's current
-    stream on the current device (so torch events time our launches)."""
+    stream on `device` (the current device when None), so torch events time
+    our launches."""
     if stream is None:
         t = _lib.torch
         if t is not None and t.cuda.is_available():
-            return int(t.cuda.current_stream().cuda_stream)
+            cs = t.cuda.current_stream() if device is None else t.cuda.current_stream(device)
+            return int(cs.cuda_stream)
         return 0
     if isinstance(stream, int):
         return stream
@@ -88,6 +90,15 @@ def _stream(stream) -> int:
 
 class Context:
     """One GPU's generator context (s3dg_ctx)."""
+
+    @classmethod
+    def _borrow(cls, handle: int, device: int) -> "Context":
+        """A context owned elsewhere (the host slot pool): never destroyed here."""
+        self = cls.__new__(cls)
+        self._h = c_vp(handle)
+        self.device = int(device)
+        self._borrowed = True
+        return self
 
     def __init__(self, device: int = 0, base_block=None, base_seed: int | None = None,
                  waves_per_block: int | None = None, nontemporal: bool = False):
@@ -106,6 +117,8 @@ class Context:
 
     # -- lifecycle -------------------------------------------------------------
     def close(self) -> None:
+        if getattr(self, "_borrowed", False):
+            return
         if getattr(self, "_h", None):
             call("s3dg_ctx_destroy", self._h)
             self._h = None
@@ -185,26 +198,47 @@ class Context:
         return out.value
 
     # -- generation (asynchronous on `stream`) ----------------------------------
+    # A torch tensor destination must live on this context's device and hold
+    # every byte the call writes (ValueError otherwise: the C ABI only sees a
+    # pointer and would write past the allocation).  A raw int pointer is the
+    # caller's responsibility.
+    def _dst(self, x, need: int) -> int:
+        p = _ptr(x)
+        if not isinstance(x, int):
+            idx = x.device.index if x.device.index is not None else 0
+            if idx != self.device:
+                raise ValueError(f"tensor is on cuda:{idx}, this context is on cuda:{self.device}")
+            have = _nbytes(x)
+            if need > have:
+                raise ValueError(f"the call writes {need} bytes, the tensor holds {have}")
+        return p
+
+    def _s(self, stream) -> int:
+        return _stream(stream, self.device)
+
     def fill_controlled(self, dst, nbytes: int | None = None, dedup: int = 1, compress=1,
                         entropy: int = 0, stream=None) -> None:
         """One object (src/data_gen.rs:151) of `nbytes` at dst."""
-        n = _nbytes(dst) if nbytes is None else nbytes
+        n = _nbytes(dst) if nbytes is None else int(nbytes)
         fn, fd = compress_ratio(compress)
-        call("s3dg_fill_controlled", self._h, _ptr(dst), int(n), int(dedup), fn, fd,
-             int(entropy) & (2**64 - 1), _stream(stream))
+        call("s3dg_fill_controlled", self._h, self._dst(dst, n), n, int(dedup), fn, fd,
+             int(entropy) & (2**64 - 1), self._s(stream))
 
     def random_data(self, dst, nbytes: int | None = None, entropy: int = 0, stream=None) -> None:
         """generate_random_data's layout (src/data_gen.rs:102-132): no zero
         prefix, one window at 0 and one at L-32 (L > 2048), seeded by `entropy`."""
-        n = _nbytes(dst) if nbytes is None else nbytes
-        call("s3dg_random_data", self._h, _ptr(dst), int(n), int(entropy) & (2**64 - 1),
-             _stream(stream))
+        n = _nbytes(dst) if nbytes is None else int(nbytes)
+        call("s3dg_random_data", self._h, self._dst(dst, n), n, int(entropy) & (2**64 - 1),
+             self._s(stream))
 
     def fill_range(self, dst, length: int, blk_lo: int, blk_hi: int, dedup: int = 1,
                    compress=1, entropy: int = 0, stream=None) -> None:
+        """Blocks [blk_lo, blk_hi) of a `length`-byte object, block blk_lo at dst."""
         fn, fd = compress_ratio(compress)
-        call("s3dg_fill_controlled_range", self._h, _ptr(dst), int(length), int(blk_lo),
-             int(blk_hi), int(dedup), fn, fd, int(entropy) & (2**64 - 1), _stream(stream))
+        hi = min(int(blk_hi) * BLOCK_SIZE, int(length))
+        need = max(0, hi - int(blk_lo) * BLOCK_SIZE)
+        call("s3dg_fill_controlled_range", self._h, self._dst(dst, need), int(length), int(blk_lo),
+             int(blk_hi), int(dedup), fn, fd, int(entropy) & (2**64 - 1), self._s(stream))
 
     def fill_stream(self, dst, obj_size: int, n_objs: int, stride: int | None = None,
                     dedup: int = 1, compress=1, seed_base: int = 0, first_obj: int = 0,
@@ -212,46 +246,58 @@ class Context:
         """n_objs equal objects, object j at dst + j*stride with entropy
         object_entropy(seed_base, first_obj + j)."""
         stride = obj_size if stride is None else stride
+        need = (int(n_objs) - 1) * int(stride) + int(obj_size) if n_objs > 0 and obj_size > 0 else 0
         fn, fd = compress_ratio(compress)
-        call("s3dg_fill_controlled_stream", self._h, _ptr(dst), int(obj_size), int(stride),
+        call("s3dg_fill_controlled_stream", self._h, self._dst(dst, need), int(obj_size), int(stride),
              int(n_objs), int(dedup), fn, fd, int(seed_base) & (2**64 - 1), int(first_obj),
-             _stream(stream))
+             self._s(stream))
 
     def fill_batch(self, dst, objects, stream=None) -> None:
         """objects: iterable of (dst_off, size, entropy, dedup, compress)."""
         objs = list(objects)
         arr = (ObjDesc * max(1, len(objs)))()
+        need = 0
         for k, (off, size, ent, dd, comp) in enumerate(objs):
             fn, fd = compress_ratio(comp)
             arr[k] = ObjDesc(int(off), int(size), int(ent) & (2**64 - 1), int(dd), fn, fd)
-        call("s3dg_fill_controlled_batch", self._h, _ptr(dst), arr, len(objs), _stream(stream))
+            if size:
+                need = max(need, int(off) + int(size))
+        call("s3dg_fill_controlled_batch", self._h, self._dst(dst, need), arr, len(objs), self._s(stream))
 
     def xoshiro_fill(self, dst, nbytes: int | None = None, chunk_bytes: int = 2 << 20,
                      seed_base: int = 0, stream=None) -> None:
         """Keystream fill, chunk k = Xoshiro256PlusPlus::seed_from_u64(seed_base + k)
         .fill_bytes(chunk) (src/data_formats/npz.rs:376-383)."""
-        n = _nbytes(dst) if nbytes is None else nbytes
-        call("s3dg_xoshiro_fill", self._h, _ptr(dst), int(n), int(chunk_bytes),
-             int(seed_base) & (2**64 - 1), _stream(stream))
+        n = _nbytes(dst) if nbytes is None else int(nbytes)
+        call("s3dg_xoshiro_fill", self._h, self._dst(dst, n), n, int(chunk_bytes),
+             int(seed_base) & (2**64 - 1), self._s(stream))
 
     def dgen_fill(self, dst, obj_size: int, blk_lo: int = 0, blk_hi: int | None = None,
                   dedup: int = 1, compress=1, seed: int = 0, stream=None) -> None:
         """DG1 blocks [blk_lo, blk_hi) of an obj_size-byte object (1 MiB blocks)."""
         fn, fd = compress_ratio(compress)
         hi = (obj_size + (1 << 20) - 1) >> 20 if blk_hi is None else blk_hi
-        call("s3dg_dgen_fill", self._h, _ptr(dst), int(obj_size), int(blk_lo), int(hi),
-             int(dedup), fn, fd, int(seed) & (2**64 - 1), _stream(stream))
+        need = max(0, min(int(hi) << 20, int(obj_size)) - (int(blk_lo) << 20))
+        call("s3dg_dgen_fill", self._h, self._dst(dst, need), int(obj_size), int(blk_lo), int(hi),
+             int(dedup), fn, fd, int(seed) & (2**64 - 1), self._s(stream))
 
     def write_ceiling(self, dst, nbytes: int | None = None, pattern: int = 0xA5A5A5A5,
                       stream=None) -> None:
-        n = _nbytes(dst) if nbytes is None else nbytes
-        call("s3dg_write_ceiling", self._h, _ptr(dst), int(n), int(pattern), _stream(stream))
+        n = _nbytes(dst) if nbytes is None else int(nbytes)
+        call("s3dg_write_ceiling", self._h, self._dst(dst, n), n, int(pattern), self._s(stream))
 
     def write_ceiling_tiled(self, dst, nbytes: int | None = None, pattern: int = 0xA5A5A5A5,
                             stream=None) -> None:
         """Store-only kernel in the tiled fill shape (batch knobs + trailing record loads)."""
-        n = _nbytes(dst) if nbytes is None else nbytes
-        call("s3dg_write_ceiling_tiled", self._h, _ptr(dst), int(n), int(pattern), _stream(stream))
+        n = _nbytes(dst) if nbytes is None else int(nbytes)
+        call("s3dg_write_ceiling_tiled", self._h, self._dst(dst, n), n, int(pattern), self._s(stream))
+
+    def write_ceiling_fill(self, dst, nbytes: int | None = None, pattern: int = 0, stream=None) -> None:
+        """The tiled fill itself with the PRNG chain and window patches compiled
+        out (s3dg_write_ceiling_fill): the fill's own store-only bound.
+        `pattern` is unused (same call shape as the other ceilings)."""
+        n = _nbytes(dst) if nbytes is None else int(nbytes)
+        call("s3dg_write_ceiling_fill", self._h, self._dst(dst, n), n, self._s(stream))
 
     def sync(self, stream=None) -> None:
         call("s3dg_sync", self._h, 0 if stream is None else _stream(stream))
@@ -268,3 +314,35 @@ def device_count() -> int:
     n = ctypes.c_int()
     call("s3dg_device_count", ctypes.byref(n))
     return n.value
+
+
+def host_slots() -> list[int]:
+    """Devices of the host-buffer drop-ins' slots (include/s3dlio_gpu.h): one
+    per visible GPU unless S3DLIO_GPU_DEVICE / S3DLIO_GPU_DEVICES say otherwise."""
+    n = ctypes.c_int()
+    call("s3dg_host_slot_count", ctypes.byref(n))
+    out = []
+    for k in range(n.value):
+        d = ctypes.c_int()
+        call("s3dg_host_slot_device", k, ctypes.byref(d))
+        out.append(d.value)
+    return out
+
+
+def host_context(slot: int = -1) -> Context:
+    """A host slot's context (borrowed: owned by the pool); slot < 0 takes the
+    next slot round-robin."""
+    h = c_vp()
+    call("s3dg_host_slot_context", int(slot), ctypes.byref(h))
+    d = ctypes.c_int()
+    call("s3dg_ctx_device", h, ctypes.byref(d))
+    return Context._borrow(h.value, d.value)
+
+
+def parse_devices(pin: str | None, lst: str | None, ndev: int) -> list[int]:
+    """The slot device list for given env values (pure; s3dg_host_parse_devices)."""
+    out = (ctypes.c_int * 64)()
+    n = ctypes.c_int()
+    call("s3dg_host_parse_devices", pin.encode() if pin is not None else None,
+         lst.encode() if lst is not None else None, int(ndev), out, 64, ctypes.byref(n))
+    return list(out[:n.value])

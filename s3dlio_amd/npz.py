@@ -8,26 +8,17 @@ is computed by the device CRC kernel, the ZIP/NPY framing on the host.
 from __future__ import annotations
 
 import ctypes
-import os
-import threading
-
 import numpy as np
 
 from . import hostbuf
 from ._lib import c_u32, c_u64, call, lib
-from .device import Context, _ptr, _stream
-
-_ctx = None
-_lock = threading.Lock()
-
+from .device import Context, _ptr, _stream, host_context
 
 def default_context() -> Context:
-    """Process-default context on env S3DLIO_GPU_DEVICE (default 0)."""
-    global _ctx
-    with _lock:
-        if _ctx is None:
-            _ctx = Context(int(os.environ.get("S3DLIO_GPU_DEVICE", "0")))
-        return _ctx
+    """The next host slot's context, round-robin (include/s3dlio_gpu.h host
+    slots: every visible GPU unless S3DLIO_GPU_DEVICE / S3DLIO_GPU_DEVICES
+    say otherwise); borrowed from the pool."""
+    return host_context(-1)
 
 
 def _shape_arr(shape):

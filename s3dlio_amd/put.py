@@ -23,6 +23,7 @@ fill_controlled_data layout instead (the benchmark kernel).
 from __future__ import annotations
 
 import ctypes
+import threading
 import os
 import time
 from dataclasses import dataclass, field
@@ -78,24 +79,22 @@ def _contexts(devices):
     """Contexts for `devices`: None / "all" = every visible GPU, else a list of
     device indices (repeats give several lanes on one GPU)."""
     from .device import Context
-    from .npz import default_context
     if devices is None or devices == "all":
         n = ctypes.c_int()
         call("s3dg_device_count", ctypes.byref(n))
         devices = list(range(max(1, n.value)))
     ctxs = []
     for d in devices:
-        if d == 0 and not any(c.device == 0 for c in ctxs):
-            ctxs.append(default_context())
-        else:
-            key = (int(d), sum(1 for c in ctxs if c.device == int(d)))
+        key = (int(d), sum(1 for c in ctxs if c.device == int(d)))
+        with _LANE_LOCK:
             if key not in _LANE_CTX:
                 _LANE_CTX[key] = Context(int(d))
             ctxs.append(_LANE_CTX[key])
     return ctxs
 
 
-_LANE_CTX: dict = {}
+_LANE_CTX: dict = {}      # (device, lane) -> Context, kept for the process
+_LANE_LOCK = threading.Lock()
 
 
 def put_objects(uris, size: int, max_in_flight: int = 64, config: Config | None = None,

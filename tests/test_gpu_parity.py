@@ -187,8 +187,8 @@ def test_large_random_data_tiled(gpu_ctx, torch, oracle, base, L, off):
 
 def test_tile_map_shared_across_streams(gpu_ctx, torch, oracle, base):
     """A batch on one stream and a tiled stream on another, back to back with
-    no host sync: both read the context's tile map, so the second k_tile_map
-    must wait for the first fill (tile_free event).  Repeated with growth."""
+    no host sync: each stream has its own tile map and batch staging, so the
+    two launches share nothing.  Repeated with growth."""
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     rnd = random.Random(99)
     for rep in range(3):
@@ -380,7 +380,7 @@ def test_invalid_arguments_raise(gpu_ctx, torch):
         gpu_ctx.fill_controlled(int(t.data_ptr()) + 1, 100)
     with pytest.raises(ValueError):
         gpu_ctx.fill_stream(t, obj_size=4096, n_objs=2, stride=100)
-    for bad in (1, 4, 9, 128):
+    for bad in (2, 4, 9, 128):
         with pytest.raises(ValueError, match="tile"):
             gpu_ctx.set_batch_tile(bad)
 
