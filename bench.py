@@ -478,8 +478,13 @@ def ceilings(torch, ctx, ring, stream, args, store) -> dict:
     occ = -1 if args.occupancy is None else args.occupancy
     ctx.set_occupancy(occ, occ)
     ctx.set_store_policy(store, store)
-    fill_ceiling = round(rate(ctx.write_ceiling_fill), 1)
-    shapes = {}
+    # the ablated fill at several store pacings (wave-0 delay where the fill
+    # plans); the best is the ceiling
+    paced = {pace: round(rate(lambda b, n, stream, pace=pace: ctx.write_ceiling_fill(b, n, pace=pace, stream=stream)), 1)
+             for pace in (0, 2, 4, 8, 16)}
+    best_pace = max(paced, key=paced.get)
+    fill_ceiling = paced[best_pace]
+    shapes = {f"ablated_fill_pace{p_}": v for p_, v in paced.items()}
     names = {-1: "default", 0: "plain", 1: "nt", 2: "sc1", 3: "ntsc1"}
     shapes[f"tiled_1w_{ctx.query_occupancy(batch=True)}perCU_{names[store]}"] = round(
         rate(ctx.write_ceiling_tiled), 1)
@@ -495,8 +500,8 @@ def ceilings(torch, ctx, ring, stream, args, store) -> dict:
         assert hip.hipMemsetD32Async(buf.data_ptr(), 0x5A5A5A5A, nbytes // 4, int(stream.cuda_stream)) == 0
     shapes["hipMemsetD32Async"] = round(rate(memset_d32), 1)
     return {"write_ceiling_GBps": fill_ceiling,
-            "write_ceiling_kind": "k_fill_batch with the PRNG chain and window patches compiled out "
-                                  "(s3dg_write_ceiling_fill), 8 MiB objects",
+            "write_ceiling_kind": f"k_fill_batch with the PRNG chain and window patches compiled out "
+                                  f"(s3dg_write_ceiling_fill), 8 MiB objects, best pacing {best_pace}",
             "store_only_shapes_GBps": shapes}
 
 
@@ -632,9 +637,10 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes):
     kind = cfg["kind"]
     meta = {"cores": threads, "kind": "port", "affinity_cpus": share["affinity_cpus"],
             "cgroup_quota_cpus": share["cgroup_quota_cpus"]}
-    if kind in ("stream", "single"):
+    if kind in ("stream", "single") or (kind == "batch" and cfg.get("uniform")):
         # fill_controlled_data's par_chunks_mut(4096) over a reused 1 GiB ring
-        size = cfg["size"]
+        # (uniform batches: the same objects, laid out back to back)
+        size = cfg["size"] or cfg["uniform"]
         per = max(1, GiB // size)
         buf = np.ones(per * size, np.uint8)                        # fault the pages in before timing
         OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, 0, base, threads=threads, out=buf)
@@ -650,7 +656,7 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes):
         OC.fill_stream(size, per, cfg["dedup"], fn, fd, SEED_BASE, 0, base, threads=1, out=buf)
         one = per * size / (time.perf_counter() - t1s) / GiB
         return dict(meta, value=round(done * size / dt / GiB, 2), unit="GiB/s", single_thread_GiBps=round(one, 2),
-                    sample=f"{done} x {size // KiB} KiB objects ({done * size / GiB:.0f} GiB) over {dt:.1f} s into "
+                    sample=f"{done} x {size / KiB:g} KiB objects ({done * size / GiB:.0f} GiB) over {dt:.1f} s into "
                            f"a reused 1 GiB host ring, {threads} threads over 4 KiB blocks; {cpu_model()}")
     # per-object (or per-chunk) tasks from a pool of host threads, each thread
     # writing its own reused host ring

@@ -172,8 +172,10 @@ int s3dg_write_ceiling_tiled(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pa
  * tile records, grid, LDS image, barrier, stores and trailing record loads)
  * with the PRNG chain and the window patches compiled out.  Its bytes are
  * meaningless; it is the write ceiling the fill is measured against.
+ * pace > 0 makes wave 0 of every workgroup idle pace x 128 cycles where the
+ * fill plans its block (store issue paced like the fill's).
  * len < 8 MiB or a multiple of 8 MiB. */
-int s3dg_write_ceiling_fill(s3dg_ctx *ctx, void *dst, uint64_t len, void *stream);
+int s3dg_write_ceiling_fill(s3dg_ctx *ctx, void *dst, uint64_t len, uint32_t pace, void *stream);
 
 /* ---- memory / copy helpers ------------------------------------------------ */
 int s3dg_device_alloc(s3dg_ctx *ctx, uint64_t bytes, void **out);

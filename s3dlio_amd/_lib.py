@@ -75,7 +75,7 @@ SIGNATURES = {
     "s3dg_fill_controlled_batch": (c_int, [c_vp, c_vp, ctypes.POINTER(ObjDesc), c_u64, c_vp]),
     "s3dg_write_ceiling": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
     "s3dg_write_ceiling_tiled": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
-    "s3dg_write_ceiling_fill": (c_int, [c_vp, c_vp, c_u64, c_vp]),
+    "s3dg_write_ceiling_fill": (c_int, [c_vp, c_vp, c_u64, c_u32, c_vp]),
     "s3dg_xoshiro_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_vp]),
     "s3dg_xoshiro_jump": (c_int, [ctypes.POINTER(c_u64), c_u64]),
     "s3dg_dgen_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),

@@ -18,9 +18,13 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -547,6 +551,132 @@ int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {
 constexpr uint64_t kBatchSubFirst = 16384, kBatchSubMax = 262144;
 // relative costs in units of one live 4 KiB block
 constexpr double kDeadSlotCost = 0.25, kRecordCost = 0.1;
+constexpr int kPrepParts = 4;                   // host threads per sub-batch pass
+constexpr uint64_t kPrepMinPerPart = 8192;      // descriptors below which a pass stays single-threaded
+
+// A few persistent host threads for the batch passes: run(parts, fn) calls
+// fn(0..parts-1), part 0 in the caller.  One run at a time; a second caller
+// meanwhile runs its parts itself.
+class PrepPool {
+public:
+    static PrepPool &get() {
+        static PrepPool *p = new PrepPool();   // never destroyed: workers outlive main
+        return *p;
+    }
+    void run(int parts, const std::function<void(int)> &fn) {
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock() || parts <= 1) {
+            for (int q = 0; q < parts; ++q) fn(q);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            parts_ = parts;
+            next_.store(1);
+            left_ = parts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        for (int q; (q = next_.fetch_add(1)) < parts;) finish_one(q);
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [&] { return left_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    PrepPool() {
+        for (int k = 0; k < kPrepParts - 1; ++k) std::thread([this] { loop(); }).detach();
+    }
+    void finish_one(int q) {
+        (*fn_)(q);
+        std::lock_guard<std::mutex> g(mu_);
+        if (--left_ == 0) done_cv_.notify_all();
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+            }
+            for (int q; (q = next_.fetch_add(1)) < parts_;) finish_one(q);
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)> *fn_ = nullptr;
+    int parts_ = 0, left_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+};
+
+// Pass 1 over descriptors [k0, k1): validation, slot counts per tile size,
+// dense-layout test.
+struct BatchScan {
+    uint64_t m = 0, blocks = 0, ntiles[kTileShiftMax + 1] = {};
+    uint64_t first_off = 0, last_end = 0;
+    bool dense_ok = true;
+    int err = S3DG_OK;
+    const char *msg = nullptr;
+};
+
+static void batch_scan(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P) {
+    for (uint64_t k = k0; k < k1; ++k) {
+        const s3dg_obj_desc &o = d[k];
+        if (o.size == 0) continue;
+        if (o.dst_off & 15u) { P.err = S3DG_EINVAL; P.msg = "dst_off must be a multiple of 16"; return; }
+        if (o.f_den == 0 || o.f_num >= o.f_den) { P.err = S3DG_EINVAL; P.msg = "need f_num < f_den"; return; }
+        const uint64_t nb = (o.size + kBlk - 1) / kBlk;
+        if (nb >= (1ull << 31)) { P.err = S3DG_EINVAL; P.msg = "object larger than 2^31 blocks"; return; }
+        const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
+        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
+            P.ntiles[sh] += (nb + lead + (1ull << sh) - 1) >> sh;
+        if (P.m == 0) P.first_off = o.dst_off;
+        else if (o.dst_off < P.last_end) P.dense_ok = false;
+        if (o.dst_off & (kBlk - 1)) P.dense_ok = false;
+        P.last_end = o.dst_off + nb * kBlk;
+        P.blocks += nb;
+        ++P.m;
+    }
+}
+
+// Pass 2: entries j0.. of [k0, k1) with their record ranges, records from rec0
+// (tile layouts) or per granule from lead0 + (dst_off - first_off) / 4 KiB (dense).
+// In the dense layout an entry's rec_hi is the next object's first granule;
+// the caller patches the last entry of every part.
+static void batch_write(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr_t base, uint32_t tshift,
+                        uint64_t lead0, uint64_t first_off, uint64_t j0, uint64_t rec0, BatchEnt *out) {
+    uint64_t rec = rec0, j = j0;
+    for (uint64_t k = k0; k < k1; ++k) {
+        const s3dg_obj_desc &o = d[k];
+        if (o.size == 0) continue;
+        const uint64_t nb = (o.size + kBlk - 1) / kBlk;
+        BatchEnt &e = out[j];
+        e.dst_off = o.dst_off;
+        e.size = o.size;
+        e.entropy = o.entropy;
+        e.dedup = o.dedup;
+        e.f_num = o.f_num;
+        e.f_den = o.f_den;
+        if (tshift == 0) {
+            const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
+            e.blk0 = g0;
+            e.rec_lo = j == 0 ? 0 : g0;
+            if (j > j0) out[j - 1].rec_hi = g0;   // the gap before this object: dead records
+            e.rec_hi = g0 + nb;
+        } else {
+            const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
+            e.rec_lo = rec;
+            rec += (nb + lead + (1ull << tshift) - 1) >> tshift;
+            e.rec_hi = rec;
+            e.blk0 = (e.rec_lo << tshift) + lead;
+        }
+        ++j;
+    }
+}
 
 int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc *d, uint64_t n,
                                void *stream) {
@@ -563,45 +693,48 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     for (auto &G : S->stage)
         for (hipEvent_t *ev : {&G.uploaded, &G.consumed})
             if (!*ev) HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "hipEventCreate");
+    PrepPool &pool = PrepPool::get();
     uint64_t sub = kBatchSubFirst;
     for (uint64_t k0 = 0; k0 < n;) {
         const uint64_t k1 = n - k0 < sub ? n : k0 + sub;
         sub = sub * 2 < kBatchSubMax ? sub * 2 : kBatchSubMax;
-        // pass 1: validate, count slots per tile size, test the dense layout
-        uint64_t m = 0, blocks = 0, ntiles[kTileShiftMax + 1] = {};
-        uint64_t first_off = 0, prev_end = 0;
-        bool dense_ok = true;
-        for (uint64_t k = k0; k < k1; ++k) {
-            const s3dg_obj_desc &o = d[k];
-            if (o.size == 0) continue;
-            if (o.dst_off & 15u) return fail(S3DG_EINVAL, "dst_off must be a multiple of 16");
-            if (o.f_den == 0 || o.f_num >= o.f_den) return fail(S3DG_EINVAL, "need f_num < f_den");
-            const uint64_t nb = (o.size + kBlk - 1) / kBlk;
-            if (nb >= (1ull << 31)) return fail(S3DG_EINVAL, "object larger than 2^31 blocks");
-            const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
-            for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
-                ntiles[sh] += (nb + lead + (1ull << sh) - 1) >> sh;
-            if (m == 0) first_off = o.dst_off;
-            else if (o.dst_off < prev_end) dense_ok = false;
-            if (o.dst_off & (kBlk - 1)) dense_ok = false;
-            prev_end = o.dst_off + nb * kBlk;
-            blocks += nb;
-            ++m;
+        // pass 1 in parts, then merged in order
+        int parts = (int)((k1 - k0) / kPrepMinPerPart);
+        parts = parts < 1 ? 1 : (parts > kPrepParts ? kPrepParts : parts);
+        uint64_t cut[kPrepParts + 1];
+        for (int q = 0; q <= parts; ++q) cut[q] = k0 + (k1 - k0) * (uint64_t)q / (uint64_t)parts;
+        BatchScan part[kPrepParts];
+        pool.run(parts, [&](int q) { batch_scan(d, cut[q], cut[q + 1], base, part[q]); });
+        BatchScan P;
+        for (int q = 0; q < parts; ++q) {
+            const BatchScan &Q = part[q];
+            if (Q.err) return fail(Q.err, Q.msg);
+            if (Q.m == 0) continue;
+            if (P.m == 0) P.first_off = Q.first_off;
+            else if (Q.first_off < P.last_end) P.dense_ok = false;
+            P.dense_ok = P.dense_ok && Q.dense_ok;
+            P.last_end = Q.last_end;
+            P.m += Q.m;
+            P.blocks += Q.blocks;
+            for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles[sh] += Q.ntiles[sh];
         }
+        const uint64_t m = P.m;
         if (m == 0) { k0 = k1; continue; }
-        const uint64_t lead0 = ((base + first_off) >> 12) & 7;
-        const uint64_t span = dense_ok ? lead0 + (prev_end - first_off) / kBlk : 0;
+        const uint64_t lead0 = ((base + P.first_off) >> 12) & 7;
+        const uint64_t span = P.dense_ok ? lead0 + (P.last_end - P.first_off) / kBlk : 0;
         // layout: forced (s3dg_set_batch_tile) or least cost
         uint32_t tshift = kTileShiftMax;
-        if (c->tile_shift == 0 && c->tile_force_dense && dense_ok) tshift = 0;
+        if (c->tile_shift == 0 && c->tile_force_dense && P.dense_ok) tshift = 0;
         else if (c->tile_shift) tshift = c->tile_shift;
         else {
             double best = 1e300;
             for (uint32_t sh = kTileShiftMax; sh >= kTileShiftMin; --sh) {
-                const double cost = kDeadSlotCost * (double)((ntiles[sh] << sh) - blocks) + kRecordCost * ntiles[sh];
+                const double cost =
+                    kDeadSlotCost * (double)((P.ntiles[sh] << sh) - P.blocks) + kRecordCost * (double)P.ntiles[sh];
                 if (cost < best) { best = cost; tshift = sh; }
             }
-            if (dense_ok && kDeadSlotCost * (double)(span - blocks) + kRecordCost * (double)span < best) tshift = 0;
+            if (P.dense_ok && kDeadSlotCost * (double)(span - P.blocks) + kRecordCost * (double)span < best)
+                tshift = 0;
         }
         // staging: host buffer free once its last upload finished, device copy
         // once the k_batch_map that read it finished
@@ -619,35 +752,20 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             HIP_TRY(hipMalloc((void **)&G.dev, cap * sizeof(BatchEnt)), "hipMalloc(batch staging)");
             G.cap = cap;
         }
-        // pass 2: the entries and their record ranges
-        uint64_t rec = 0, j = 0;
-        for (uint64_t k = k0; k < k1; ++k) {
-            const s3dg_obj_desc &o = d[k];
-            if (o.size == 0) continue;
-            const uint64_t nb = (o.size + kBlk - 1) / kBlk;
-            BatchEnt &e = G.host[j];
-            e.dst_off = o.dst_off;
-            e.size = o.size;
-            e.entropy = o.entropy;
-            e.dedup = o.dedup;
-            e.f_num = o.f_num;
-            e.f_den = o.f_den;
-            if (tshift == 0) {
-                const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
-                e.blk0 = g0;
-                e.rec_lo = j == 0 ? 0 : g0;
-                if (j > 0) G.host[j - 1].rec_hi = g0;   // the gap before this object: dead records
-                e.rec_hi = g0 + nb;
-            } else {
-                const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
-                e.rec_lo = rec;
-                rec += (nb + lead + (1ull << tshift) - 1) >> tshift;
-                e.rec_hi = rec;
-                e.blk0 = (e.rec_lo << tshift) + lead;
-            }
-            ++j;
+        // pass 2 in the same parts: entry and record offsets from the part counts
+        uint64_t j0[kPrepParts], rec0[kPrepParts];
+        for (int q = 0; q < parts; ++q) {
+            j0[q] = q ? j0[q - 1] + part[q - 1].m : 0;
+            rec0[q] = q ? rec0[q - 1] + (tshift ? part[q - 1].ntiles[tshift] : 0) : 0;
         }
-        const uint64_t recs = tshift == 0 ? span : rec;
+        BatchEnt *H = G.host;
+        pool.run(parts, [&](int q) {
+            batch_write(d, cut[q], cut[q + 1], base, tshift, lead0, P.first_off, j0[q], rec0[q], H);
+        });
+        if (tshift == 0)     // a part's last object ends where the next part's first begins
+            for (int q = 1; q < parts; ++q)
+                if (part[q].m && j0[q]) H[j0[q] - 1].rec_hi = H[j0[q]].blk0;
+        const uint64_t recs = tshift == 0 ? span : rec0[parts - 1] + part[parts - 1].ntiles[tshift];
         if (int r = tiles_reserve(S, recs, s)) return r;
         HIP_TRY(hipStreamWaitEvent(S->up, G.consumed, 0), "hipStreamWaitEvent");
         HIP_TRY(hipMemcpyAsync(G.dev, G.host, m * sizeof(BatchEnt), hipMemcpyHostToDevice, S->up),
@@ -825,7 +943,7 @@ int s3dg_write_ceiling_tiled(s3dg_ctx *c, void *dst, uint64_t len, uint32_t patt
     return S3DG_OK;
 }
 
-int s3dg_write_ceiling_fill(s3dg_ctx *c, void *dst, uint64_t len, void *stream) {
+int s3dg_write_ceiling_fill(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pace, void *stream) {
     CTX_SCOPE(c);
     if (!dst || !aligned16(dst) || (len % kBlk))
         return fail(S3DG_EINVAL, "dst must be 16-byte aligned and len a multiple of 4096");
@@ -845,7 +963,9 @@ int s3dg_write_ceiling_fill(s3dg_ctx *c, void *dst, uint64_t len, void *stream) 
     StreamState *S = stream_state(c, s);
     std::lock_guard<std::mutex> g(S->mu);
     if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
-    HIP_TRY(launch_fill_uniform_tiles_ablated(cfg_for(c, true), (uint8_t *)dst, obj, kObj, n_objs, (uint32_t)tpo,
+    LaunchCfg lc = cfg_for(c, true);
+    lc.pace = pace;
+    HIP_TRY(launch_fill_uniform_tiles_ablated(lc, (uint8_t *)dst, obj, kObj, n_objs, (uint32_t)tpo,
                                               tshift, lead, pp, S->tiles, c->base_dev, s),
             "launch k_fill_batch(ablated)");
     return S3DG_OK;

@@ -72,6 +72,7 @@ struct LaunchCfg {
     int waves_per_block;   // 1, 2 or 4 wave64s per 4 KiB block (one workgroup)
     uint32_t dyn_lds = 0;  // reserved dynamic LDS per workgroup (occupancy cap)
     uint32_t prefetch_tiles = 0;   // batch: tile-record prefetch distance (0 = off)
+    uint32_t pace = 0;             // store-only reference only: wave-0 delay before the stores
 };
 
 // Dynamic LDS that caps a fill launch at `wgs` resident workgroups per CU

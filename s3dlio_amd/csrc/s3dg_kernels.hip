@@ -318,7 +318,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 template <int NT, int NW, bool ABL = false>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
-                                                        uint32_t tshift, const u32x4 *base) {
+                                                        uint32_t tshift, const u32x4 *base, uint32_t pace) {
     __shared__ __attribute__((aligned(16))) BlockLds S;
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -340,6 +340,10 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     const int64_t ib = (int64_t)e.first + k - e.lead;
     uint8_t *const bdst = dst_base + e.dst_off + (uint64_t)ib * kBlk;
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
+    if constexpr (ABL) {   // store-only reference: wave 0 idles `pace` x 2 x 64 cycles in the plan's place
+        if (wave == 0)
+            for (uint32_t q = 0; q < pace; ++q) __builtin_amdgcn_s_sleep(2);
+    }
     gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
@@ -718,13 +722,14 @@ void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const u3
 template <int NT, int NW>
 void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
                       uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b);
+    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b, 0u);
 }
 
 template <int NT, int NW>
 void launch_batch_abl_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
-                          uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b);
+                          uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b, uint32_t pace) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b,
+                       pace);
 }
 
 template <int NT, int NW>
@@ -816,7 +821,7 @@ static hipError_t batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t t
         const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
         if (ablated)
             S3DG_DISPATCH(launch_batch_abl_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
-                          lc.prefetch_tiles, tshift, b);
+                          lc.prefetch_tiles, tshift, b, lc.pace);
         else
             S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
                           lc.prefetch_tiles, tshift, b);

@@ -292,12 +292,12 @@ class Context:
         n = _nbytes(dst) if nbytes is None else int(nbytes)
         call("s3dg_write_ceiling_tiled", self._h, self._dst(dst, n), n, int(pattern), self._s(stream))
 
-    def write_ceiling_fill(self, dst, nbytes: int | None = None, pattern: int = 0, stream=None) -> None:
+    def write_ceiling_fill(self, dst, nbytes: int | None = None, pace: int = 0, stream=None) -> None:
         """The tiled fill itself with the PRNG chain and window patches compiled
-        out (s3dg_write_ceiling_fill): the fill's own store-only bound.
-        `pattern` is unused (same call shape as the other ceilings)."""
+        out (s3dg_write_ceiling_fill): the fill's own store-only bound; `pace`
+        delays wave 0 by pace x 128 cycles where the fill plans its block."""
         n = _nbytes(dst) if nbytes is None else int(nbytes)
-        call("s3dg_write_ceiling_fill", self._h, self._dst(dst, n), n, self._s(stream))
+        call("s3dg_write_ceiling_fill", self._h, self._dst(dst, n), n, int(pace), self._s(stream))
 
     def sync(self, stream=None) -> None:
         call("s3dg_sync", self._h, 0 if stream is None else _stream(stream))

@@ -64,8 +64,9 @@ def main():
     cb = n8 * 8 * MiB
     W["ceil_tiled"] = (lambda: call("s3dg_write_ceiling_tiled", ctx._h, base, cb, 0xA5A5A5A5, sh), cb, 1)
     W["ceil"] = (lambda: call("s3dg_write_ceiling", ctx._h, base, cb, 0xA5A5A5A5, sh), cb, 1)
-    if True:
-        W["ceil_fill"] = (lambda: call("s3dg_write_ceiling_fill", ctx._h, base, cb, sh), cb, 1)
+    W["ceil_fill"] = (lambda: call("s3dg_write_ceiling_fill", ctx._h, base, cb, 0, sh), cb, 1)
+    for pace in (1, 2, 3, 4, 6, 8, 12, 16):
+        W[f"ceil_fill_p{pace}"] = (lambda pace=pace: call("s3dg_write_ceiling_fill", ctx._h, base, cb, pace, sh), cb, 1)
     crc_n = min(16 * GiB, cap)
     out = ctypes.c_uint32()
     W["crc"] = (lambda: call("s3dg_crc32", ctx._h, base, crc_n, sh, ctypes.byref(out)), crc_n, 1)
