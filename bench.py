@@ -302,10 +302,10 @@ def main() -> int:
              and all(b // cfg["size"] * ((cfg["size"] + 4095) // 4096) >= 16384 for _, b in launches)
              and cfg["size"] % (32 * KiB) == 0)
     if kind == "keystream":
-        kernel, launch_shape = "k_keystream", ("k_keystream<64,4>: 128 lanes x 2048 draws per 2 MiB chunk "
+        kernel, launch_shape = "k_keystream", ("k_keystream<64,4>: 256 lanes x 1024 draws per 2 MiB chunk "
                                                "(jump-ahead), 64-draw LDS stage per lane, 512-B row pieces per store")
     elif kind == "dgen":
-        kernel, launch_shape = "k_keystream (DG1 mode)", ("k_keystream<16,2>: 1024 draws per lane, 128 lanes per "
+        kernel, launch_shape = "k_keystream (DG1 mode)", ("k_keystream<64,4>: 1024 draws per lane, 128 lanes per "
                                                           "1 MiB DG1 block, zero-prefix waves skip the PRNG")
     else:
         batch = kind == "batch" or tiled
@@ -410,7 +410,7 @@ def main() -> int:
                        else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
                        "stores": (args.store if args.store != "default"
-                                  else {"keystream": "sc1", "dgen": "plain"}.get(kind, "sc1" if kind == "batch"
+                                  else {"keystream": "sc1", "dgen": "sc1"}.get(kind, "sc1" if kind == "batch"
                                                                                   or tiled else "nt sc1"))},
             "roofline": roof,
             "cpu_baseline": cpu,

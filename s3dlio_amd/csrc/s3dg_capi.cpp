@@ -35,13 +35,15 @@ constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident wo
 constexpr int kDefaultStreamTiles = 1;
 constexpr uint64_t kStreamTilesMinBlocks = 16384;   // smaller streams: 2D kernel, no tile-map launch
 constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
-constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 1024};   // npz keystream, DG1
+constexpr uint64_t kDefaultKsMinDraws[2] = {1024, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
-// measured on MI355X (tools/k2_lab.py): 512-B row pieces and sc1 stores for
-// the plain keystream; 128-B pieces, 2-wave workgroups, 1024 draws per lane
-// and plain stores for DG1 (zero-prefixed 1 MiB blocks: with 128 lanes per
-// block, whole waves fall inside the prefix and skip the PRNG)
-constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {16, 2, 0, kStorePlain}};
+// measured on MI355X (tools/k2_lab.py, profiles/r02/diag/k2_lab_r2e.log):
+// 512-B row pieces, 4-wave workgroups, 1024 draws per lane and sc1 stores for
+// both modes (K2 6010 vs 5803 GB/s at 2048 draws; DG1 c1 5933 / c2 6158 vs
+// 5187 / 5409 for the round-1 DG1 shape of 128-B pieces and 2 waves).  With
+// 1024 draws per lane a 1 MiB DG1 block is 128 lanes, so whole waves fall
+// inside a zero prefix and skip the PRNG.
+constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {64, 4, 0, kStoreSC1}};
 
 // Launch state private to one stream: the tile-record map of tiled launches
 // and the batch-descriptor staging.  Launches on one stream are ordered by

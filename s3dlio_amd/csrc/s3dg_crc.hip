@@ -63,13 +63,26 @@ struct CrcSegArgs {
     uint32_t rows;          // rows per region
 };
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // gfx950 3-input LUT op: a ^ b ^ c
+}
+
+// 20 table words per row folded by a tree of 3-input XORs: 10 VALU ops
+// instead of a serial chain of 19 two-input ones, and no long dependency
+// chain behind the row-advance lookups (PMC: the kernel is issue-bound with
+// no LDS bank conflicts, profiles/r02/diag/pmc_crc*).
 __device__ __forceinline__ uint32_t horner_row(const uint32_t (*trow)[256], const uint32_t (*tbyte)[256],
                                                uint32_t S, const uint4 v) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t c = mul_row(trow, S);
+    uint32_t t[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) c ^= tbyte[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xFF];
-    return c;
+    for (int q = 0; q < 16; ++q) t[q] = tbyte[15 - q][(w[q >> 2] >> (8 * (q & 3))) & 0xFF];
+    const uint32_t a0 = xor3(t[0], t[1], t[2]), a1 = xor3(t[3], t[4], t[5]), a2 = xor3(t[6], t[7], t[8]);
+    const uint32_t a3 = xor3(t[9], t[10], t[11]), a4 = xor3(t[12], t[13], t[14]);
+    const uint32_t b0 = xor3(a0, a1, a2), b1 = xor3(a3, a4, t[15]);
+    const uint32_t r0 = trow[0][S & 0xFF], r1 = trow[1][(S >> 8) & 0xFF], r2 = trow[2][(S >> 16) & 0xFF],
+                   r3 = trow[3][S >> 24];
+    return xor3(b0, b1, r0) ^ xor3(r1, r2, r3);
 }
 
 __global__ __launch_bounds__(256) void k_crc32_regions(CrcSegArgs a, const CrcTables *tabs,
@@ -89,12 +102,35 @@ __global__ __launch_bounds__(256) void k_crc32_regions(CrcSegArgs a, const CrcTa
     const uint32_t nrows = (uint32_t)((a.seg_rows - row0) < a.rows ? (a.seg_rows - row0) : a.rows);
     const uint4 *p = reinterpret_cast<const uint4 *>(a.src + seg * a.seg_stride + row0 * 1024) + lane;
     uint32_t S = 0, row = 0;
-    for (; row + 4 <= nrows; row += 4) {
-        uint4 v[4];
+    // Software pipelined over two register buffers: while rows r..r+3 (A) are
+    // hashed, rows r+4..r+7 (B) are in flight, then the other way round, so a
+    // wave keeps 8 KiB outstanding and every row waits only for its own load.
+    // The last loads of the loop are clamped to valid rows and not used.
+    // sched_barrier keeps the compiler from sinking the loads into the hash.
+    auto load4 = [&](uint4 (&v)[4], uint32_t r0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = p[(row + q) * 64];     // 4 rows in flight
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = r0 + q < nrows ? r0 + q : nrows - 1;
+            v[q] = p[r * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    uint4 A[4], B[4];
+    if (nrows >= 4) load4(A, 0);
+    for (; row + 8 <= nrows; row += 8) {
+        load4(B, row + 4);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, v[q]);
+        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, A[q]);
+        __builtin_amdgcn_sched_barrier(0);
+        load4(A, row + 8);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, B[q]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (row + 4 <= nrows) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, A[q]);
+        row += 4;
     }
     for (; row < nrows; ++row) S = horner_row(T.trow, T.tbyte, S, p[row * 64]);
     S = multmodp(lane_shift[lane], S);              // A^(16 (63 - lane))

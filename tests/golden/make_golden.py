@@ -34,6 +34,18 @@ KAT = {
     "splitmix64_state0": ["0xe220a8397b1dcdaf", "0x6e789e6aa1b965f4",
                           "0x06c45d188009454f", "0xf88bb8a8724c81ec"],
     "xoshiro256pp_state_1234": [41943041, 58720359, 3588806011781223, 3591011842654386],
+    # the ten values of the `reference` test of rand_xoshiro 0.7's (and rand
+    # 0.9's) Xoshiro256PlusPlus (from_seed of the little-endian words 1,2,3,4;
+    # values produced by the xoshiro256plusplus.c reference implementation)
+    "xoshiro256pp_state_1234_x10": [41943041, 58720359, 3588806011781223, 3591011842654386,
+                                    9228616714210784205, 9973669472204895162, 14011001112246962877,
+                                    12406186145184390807, 15849039046786891736, 10450023813501588000],
+    # rand 0.9's `stable_seed_from_u64` test: Xoshiro256PlusPlus::seed_from_u64(0)
+    # (the SmallRng seeding path of src/data_gen.rs:203), ten next_u64 outputs
+    "rand_seed_from_u64_0_x10": [5987356902031041503, 7051070477665621255, 6633766593972829180,
+                                 211316841551650330, 9136120204379184874, 379361710973160858,
+                                 15813423377499357806, 15596884590815070553, 5439680534584881407,
+                                 1369371744833522710],
 }
 
 # (length, dedup, compress, entropy) — compress is an int or a (p, q) ratio

@@ -477,3 +477,24 @@ def test_launch_splitting_large_grids(gpu_ctx, torch, oracle, base):
         assert np.array_equal(out[6 * stride:6 * stride + osz].cpu().numpy(), exp), waves
         del out, exp
     gpu_ctx.set_waves_per_block(0)
+
+
+def test_block_windows_equal_rand_crate_vectors(gpu_ctx, torch):
+    """Pinned without the oracle: block 0 at entropy 0 is seeded
+    SmallRng::seed_from_u64(0) (src/data_gen.rs:202-203), so its two 32-byte
+    windows (:217, :220) are next_u64 outputs 0-3 and 4-7 of rand 0.9's own
+    `stable_seed_from_u64` test, little-endian; block 1 at entropy 2^64-1 is
+    seed 0 again (u + E wraps)."""
+    kat = load("kat.json")["rand_seed_from_u64_0_x10"]
+    want1 = b"".join(v.to_bytes(8, "little") for v in kat[:4])
+    want2 = b"".join(v.to_bytes(8, "little") for v in kat[4:8])
+    t = torch.empty(2 * 4096, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_controlled(t, 4096, dedup=1, compress=1, entropy=0)
+    torch.cuda.synchronize()
+    h = bytes(t[:4096].cpu().numpy())
+    assert h[:32] == want1 and h[2048:2080] == want2
+    u = torch.empty(2 * 4096, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_controlled(u, 2 * 4096, dedup=1, compress=1, entropy=2**64 - 1)
+    torch.cuda.synchronize()
+    h = bytes(u[4096:].cpu().numpy())
+    assert h[:32] == want1 and h[2048:2080] == want2

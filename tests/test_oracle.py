@@ -35,6 +35,20 @@ def test_kat_xoshiro256pp(oracle):
         kat["xoshiro256pp_seed_from_u64_0"]
 
 
+def test_kat_rand_crate_vectors(oracle):
+    """Ten-value known answers from the rand crates' own tests (rand_xoshiro
+    0.7 / rand 0.9 Xoshiro256PlusPlus `reference` and rand 0.9
+    `stable_seed_from_u64`; the crates are not in the checkout, the values
+    are restated in tests/golden/make_golden.py).  The second pins the
+    seed_from_u64 (SplitMix64) + next_u64 path every block seed of
+    src/data_gen.rs:203 takes, in both oracles and the library's host jump."""
+    kat = load("kat.json")
+    assert oracle.xoshiro_stream([1, 2, 3, 4], 10) == kat["xoshiro256pp_state_1234_x10"]
+    assert oracle.xoshiro_seeded_stream(0, 10) == kat["rand_seed_from_u64_0_x10"]
+    r = P.Xoshiro256pp.seed_from_u64(0)
+    assert [r.next_u64() for _ in range(10)] == kat["rand_seed_from_u64_0_x10"]
+
+
 def test_fill_bytes_tail_rule():
     """1..4-byte tails take next_u32 = high half of next_u64 (rand_core 0.9)."""
     kat = load("kat.json")

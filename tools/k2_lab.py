@@ -31,15 +31,17 @@ def main():
     def run(kind):
         if kind == "k2":
             call("s3dg_xoshiro_fill", ctx._h, buf.data_ptr(), n, 2 * MiB, 0, sh)
-        else:   # DG1: one object, 1 MiB blocks, dedup 1, compress 2
+        elif kind == "dg1":   # DG1: one object, 1 MiB blocks, dedup 1, compress 2
             call("s3dg_dgen_fill", ctx._h, buf.data_ptr(), n, 0, 1 << 40, 1, 1, 2, 12345, sh)
+        else:                 # DG1 at compress 1 (no zero prefix)
+            call("s3dg_dgen_fill", ctx._h, buf.data_ptr(), n, 0, 1 << 40, 1, 0, 1, 12345, sh)
     res, occ = {}, {}
     for rep in range(int(os.environ.get("LAB_REPS", "3"))):
         for p in pts:
             ctx.set_keystream_shape(0, *p)
             ctx.set_keystream_shape(1, *p)
             occ[p] = ctx.query_keystream_occupancy(0)
-            for kind in ("k2", "dg1"):
+            for kind in os.environ.get("LAB_K2KINDS", "k2,dg1").split(","):
                 run(kind)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st); run(kind); e1.record(st); torch.cuda.synchronize()
