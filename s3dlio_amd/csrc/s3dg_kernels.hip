@@ -347,14 +347,23 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
-    // 128-byte line (2 records) of the span's records (and the (q+64k)-th
-    // with one record per block, tshift 0: 128 lines)
+    // 128-byte line (2 records) of the span's records
     constexpr uint32_t kPfSpan = 256;
     const uint32_t span = kPfSpan > (2u << tshift) ? kPfSpan : (2u << tshift);
-    const uint32_t lines = tshift ? span >> (tshift + 1) : span >> 1;
     if (pf && (g & (span - 1)) < 8) {
-        for (uint32_t q = t; q < lines; q += 64 * NW) {
-            const uint64_t pt = (((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift) + 2 * q;
+        const uint64_t first = ((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift;
+        if (tshift == 0) {
+            // one record per block: this workgroup's XCD (g mod 8, dealt
+            // round-robin) uses only the records = g (mod 8) of the span, so
+            // it touches those 32 and leaves the rest to the other XCDs
+            if (t < span / 8) {
+                const uint64_t pt = first + 8 * t + (g & 7);
+                const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
+                uint32_t dummy;
+                asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
+            }
+        } else if (t < (span >> (tshift + 1))) {
+            const uint64_t pt = first + 2 * t;
             const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
             uint32_t dummy;
             asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
