@@ -52,14 +52,21 @@ constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {64, 4, 0, kStore
 // wait on each other.
 struct StreamState {
     std::mutex mu;                     // one enqueuing thread per stream at a time
-    TileRec *tiles = nullptr;          // records (device), grown on demand
+    TileRec *tiles = nullptr;          // records of uniform tiled launches (device), grown on demand
     uint64_t tile_cap = 0;
-    hipStream_t up = nullptr;          // batch entry uploads (overlap the previous fill)
+    // batch records: two maps, so sub-batch k+1's k_batch_map (on `up`) runs
+    // while sub-batch k's fill (on the stream) reads the other one
+    TileRec *btiles[2] = {nullptr, nullptr};
+    uint64_t btile_cap[2] = {0, 0};
+    hipEvent_t mapped[2] = {nullptr, nullptr};   // map [i] written (on up)
+    hipEvent_t filled[2] = {nullptr, nullptr};   // fill reading map [i] done (on the stream)
+    int bnext = 0;
+    hipStream_t up = nullptr;          // batch entry uploads + record maps (overlap the previous fill)
     struct Stage {
         BatchEnt *host = nullptr, *dev = nullptr;   // pinned staging / device copy
         uint64_t cap = 0;
         hipEvent_t uploaded = nullptr;  // host staging may be rewritten
-        hipEvent_t consumed = nullptr;  // device copy may be overwritten (k_batch_map done)
+        hipEvent_t consumed = nullptr;  // device copy may be freed (k_batch_map done; both on `up`)
     } stage[2];
     int next = 0;
 };
@@ -263,6 +270,11 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     for (auto &kv : c->streams) {
         StreamState *S = kv.second;
         if (S->tiles) (void)hipFree(S->tiles);
+        for (int q = 0; q < 2; ++q) {
+            if (S->btiles[q]) (void)hipFree(S->btiles[q]);
+            if (S->mapped[q]) (void)hipEventDestroy(S->mapped[q]);
+            if (S->filled[q]) (void)hipEventDestroy(S->filled[q]);
+        }
         for (auto &G : S->stage) {
             if (G.host) (void)hipHostFree(G.host);
             if (G.dev) (void)hipFree(G.dev);
@@ -695,6 +707,9 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     for (auto &G : S->stage)
         for (hipEvent_t *ev : {&G.uploaded, &G.consumed})
             if (!*ev) HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "hipEventCreate");
+    for (int q = 0; q < 2; ++q)
+        for (hipEvent_t *ev : {&S->mapped[q], &S->filled[q]})
+            if (!*ev) HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "hipEventCreate");
     PrepPool &pool = PrepPool::get();
     uint64_t sub = kBatchSubFirst;
     for (uint64_t k0 = 0; k0 < n;) {
@@ -768,16 +783,30 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             for (int q = 1; q < parts; ++q)
                 if (part[q].m && j0[q]) H[j0[q] - 1].rec_hi = H[j0[q]].blk0;
         const uint64_t recs = tshift == 0 ? span : rec0[parts - 1] + part[parts - 1].ntiles[tshift];
-        if (int r = tiles_reserve(S, recs, s)) return r;
-        HIP_TRY(hipStreamWaitEvent(S->up, G.consumed, 0), "hipStreamWaitEvent");
+        // record map tb: free once the fill two sub-batches back has read it
+        const int tb = S->bnext;
+        S->bnext ^= 1;
+        if (recs > S->btile_cap[tb]) {
+            HIP_TRY(hipEventSynchronize(S->filled[tb]), "hipEventSynchronize(tile map)");
+            if (S->btiles[tb]) (void)hipFree(S->btiles[tb]);
+            S->btiles[tb] = nullptr;
+            S->btile_cap[tb] = 0;
+            const uint64_t cap = recs < 4096 ? 4096 : recs + recs / 4;
+            HIP_TRY(hipMalloc(&S->btiles[tb], cap * sizeof(TileRec)), "hipMalloc(tile map)");
+            S->btile_cap[tb] = cap;
+        }
+        // upload and map on the side stream, overlapping the previous fill
         HIP_TRY(hipMemcpyAsync(G.dev, G.host, m * sizeof(BatchEnt), hipMemcpyHostToDevice, S->up),
                 "hipMemcpyAsync(batch entries)");
         HIP_TRY(hipEventRecord(G.uploaded, S->up), "hipEventRecord");
-        HIP_TRY(hipStreamWaitEvent(s, G.uploaded, 0), "hipStreamWaitEvent");
-        HIP_TRY(launch_batch_map(G.dev, m, S->tiles, tshift, s), "launch k_batch_map");
-        HIP_TRY(hipEventRecord(G.consumed, s), "hipEventRecord");
-        HIP_TRY(launch_batch_tiles(lc, (uint8_t *)dst_base, recs, tshift, S->tiles, c->base_dev, s),
+        HIP_TRY(hipStreamWaitEvent(S->up, S->filled[tb], 0), "hipStreamWaitEvent");
+        HIP_TRY(launch_batch_map(G.dev, m, S->btiles[tb], tshift, S->up), "launch k_batch_map");
+        HIP_TRY(hipEventRecord(G.consumed, S->up), "hipEventRecord");
+        HIP_TRY(hipEventRecord(S->mapped[tb], S->up), "hipEventRecord");
+        HIP_TRY(hipStreamWaitEvent(s, S->mapped[tb], 0), "hipStreamWaitEvent");
+        HIP_TRY(launch_batch_tiles(lc, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
                 "launch k_fill_batch");
+        HIP_TRY(hipEventRecord(S->filled[tb], s), "hipEventRecord");
         k0 = k1;
     }
     return S3DG_OK;

@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void k_crc32_regions(CrcSegArgs a, const CrcTa
         for (uint32_t k = t; k < sizeof(CrcTables) / 4; k += 256) d[k] = g[k];
     }
     __syncthreads();
+    const uint32_t (*trow)[256] = T.trow;
     const uint64_t r = (uint64_t)blockIdx.x * 4 + (t >> 6);
     if (r >= a.nreg) return;
     const uint64_t seg = r / a.regs_per_seg, k = r - seg * a.regs_per_seg;
@@ -120,19 +121,19 @@ __global__ __launch_bounds__(256) void k_crc32_regions(CrcSegArgs a, const CrcTa
     for (; row + 8 <= nrows; row += 8) {
         load4(B, row + 4);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, A[q]);
+        for (int q = 0; q < 4; ++q) S = horner_row(trow, T.tbyte, S, A[q]);
         __builtin_amdgcn_sched_barrier(0);
         load4(A, row + 8);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, B[q]);
+        for (int q = 0; q < 4; ++q) S = horner_row(trow, T.tbyte, S, B[q]);
         __builtin_amdgcn_sched_barrier(0);
     }
     if (row + 4 <= nrows) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) S = horner_row(T.trow, T.tbyte, S, A[q]);
+        for (int q = 0; q < 4; ++q) S = horner_row(trow, T.tbyte, S, A[q]);
         row += 4;
     }
-    for (; row < nrows; ++row) S = horner_row(T.trow, T.tbyte, S, p[row * 64]);
+    for (; row < nrows; ++row) S = horner_row(trow, T.tbyte, S, p[row * 64]);
     S = multmodp(lane_shift[lane], S);              // A^(16 (63 - lane))
 #pragma unroll
     for (int q = 32; q >= 1; q >>= 1) S ^= __shfl_xor(S, q);

@@ -50,12 +50,13 @@ def main():
         sz = (20 << 10) + 5
         n20 = min(2000000, cap // (24 << 10))
         a20 = batch([sz] * n20, 1, 0, 1)
-        W["b20k"] = (lambda: call("s3dg_fill_controlled_batch", ctx._h, base, a20, n20, sh), n20 * sz, 1)
+        W["b20k"] = (lambda a20=a20, n20=n20: call("s3dg_fill_controlled_batch", ctx._h, base, a20, n20, sh),
+                     n20 * sz, 1)
     if "s20k" in kinds:
         sz = (20 << 10) + 5
         n20 = min(2000000, cap // (24 << 10))
-        W["s20k"] = (lambda: call("s3dg_fill_controlled_stream", ctx._h, base, sz, 24 << 10, n20, 1, 0, 1,
-                                  SEED, 0, sh), n20 * sz, 1)
+        W["s20k"] = (lambda sz=sz, n20=n20: call("s3dg_fill_controlled_stream", ctx._h, base, sz, 24 << 10, n20,
+                                                 1, 0, 1, SEED, 0, sh), n20 * sz, 1)
     n8 = min(10000, cap // (8 * MiB))
     W["cfg2"] = (lambda: call("s3dg_fill_controlled_stream", ctx._h, base, 8 * MiB, 8 * MiB, n8, 1, 0, 1,
                               SEED, 0, sh), n8 * 8 * MiB, 1)
@@ -69,6 +70,10 @@ def main():
         W[f"ceil_fill_p{pace}"] = (lambda pace=pace: call("s3dg_write_ceiling_fill", ctx._h, base, cb, pace, sh), cb, 1)
     crc_n = min(16 * GiB, cap)
     out = ctypes.c_uint32()
+    if any(k.startswith("crcr") for k in kinds):   # CRC over random bytes (the keystream)
+        call("s3dg_xoshiro_fill", ctx._h, base, crc_n, 2 * MiB, 99, sh)
+        torch.cuda.synchronize()
+        W["crcr"] = (lambda: call("s3dg_crc32", ctx._h, base, crc_n, sh, ctypes.byref(out)), crc_n, 1)
     W["crc"] = (lambda: call("s3dg_crc32", ctx._h, base, crc_n, sh, ctypes.byref(out)), crc_n, 1)
     dn = min(40 * GiB, cap)
     W["dg1c1"] = (lambda: call("s3dg_dgen_fill", ctx._h, base, dn, 0, 1 << 40, 1, 0, 1, 12345, sh), dn, 1)
