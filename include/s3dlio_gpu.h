@@ -72,8 +72,9 @@ int s3dg_set_waves_per_block(s3dg_ctx *ctx, int waves);
 int s3dg_set_nontemporal(s3dg_ctx *ctx, int on);
 /* Cache policy of the fill kernels' 16-byte stores, for stream and batch
  * launches: 0 = plain, 1 = nt, 2 = sc1, 3 = nt sc1, negative = default
- * (nt sc1 for streams, sc1 for batches, measured on MI355X).  Results are
- * identical. */
+ * (nt sc1 for streams; sc1 for tiled batch launches and nt sc1 for batch
+ * launches in the dense layout, measured on MI355X).  A non-negative batch
+ * policy applies to both batch layouts.  Results are identical. */
 int s3dg_set_store_policy(s3dg_ctx *ctx, int stream_policy, int batch_policy);
 /* Cap on resident fill workgroups per CU (reserved LDS), for stream and
  * batch launches separately; 0 = hardware maximum, negative = the default.

@@ -35,6 +35,11 @@ constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident wo
 constexpr int kDefaultStreamTiles = 1;
 constexpr uint64_t kStreamTilesMinBlocks = 16384;   // smaller streams: 2D kernel, no tile-map launch
 constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
+// dense batch layouts (one 64-B record per 4 KiB block): nt sc1 stores keep
+// the written lines out of L2, where sc1 evicts the prefetched records
+// (tools/batch_lab.py, profiles/r02/diag/batch_lab_store_*: 20 KiB+5 objects 4766 -> 6092 GB/s,
+// dense 32 KiB 5977 -> 6663, dense 64 KiB 5992 -> 6472; tiled layouts keep sc1)
+constexpr int kDefaultStoreDense = kStoreNTSC1;
 constexpr uint64_t kDefaultKsMinDraws[2] = {1024, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
 // measured on MI355X (tools/k2_lab.py, profiles/r02/diag/k2_lab_r2e.log):
@@ -77,6 +82,7 @@ struct s3dg_ctx {
     // store cache policy: sc1 (write, then drop the line from
     // L2) for batches, nt sc1 for streams, measured best
     int store_stream = kDefaultStoreStream, store_batch = kDefaultStoreBatch;
+    int store_dense = kDefaultStoreDense;   // batch launches in the dense layout
     int waves_per_block = 0;           // 0 = auto: 2 for streams, 1 for batches (measured)
     // resident fill workgroups per CU (0 = hardware max); measured on MI355X
     // (DESIGN.md §5.1): 14 for 2-wave stream blocks, no cap for 1-wave batch blocks
@@ -330,6 +336,7 @@ int s3dg_set_nontemporal(s3dg_ctx *c, int on) {
     if (!c) return fail(S3DG_EINVAL, "null context");
     c->store_stream = on ? kStoreNT : kDefaultStoreStream;
     c->store_batch = on ? kStoreNT : kDefaultStoreBatch;
+    c->store_dense = on ? kStoreNT : kDefaultStoreDense;
     return S3DG_OK;
 }
 
@@ -339,6 +346,7 @@ int s3dg_set_store_policy(s3dg_ctx *c, int stream_policy, int batch_policy) {
         return fail(S3DG_EINVAL, "store policy must be 0 (plain), 1 (nt), 2 (sc1), 3 (nt sc1) or negative (default)");
     c->store_stream = stream_policy < 0 ? kDefaultStoreStream : stream_policy;
     c->store_batch = batch_policy < 0 ? kDefaultStoreBatch : batch_policy;
+    c->store_dense = batch_policy < 0 ? kDefaultStoreDense : batch_policy;
     return S3DG_OK;
 }
 
@@ -804,7 +812,9 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         HIP_TRY(hipEventRecord(G.consumed, S->up), "hipEventRecord");
         HIP_TRY(hipEventRecord(S->mapped[tb], S->up), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(s, S->mapped[tb], 0), "hipStreamWaitEvent");
-        HIP_TRY(launch_batch_tiles(lc, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
+        LaunchCfg lcs = lc;
+        if (tshift == 0) lcs.store = c->store_dense;
+        HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
                 "launch k_fill_batch");
         HIP_TRY(hipEventRecord(S->filled[tb], s), "hipEventRecord");
         k0 = k1;
