@@ -571,8 +571,10 @@ int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {
 // Descriptors are checked per sub-batch: on an error the objects of earlier
 // sub-batches may already be enqueued.
 constexpr uint64_t kBatchSubFirst = 16384, kBatchSubMax = 262144;
-// relative costs in units of one live 4 KiB block
-constexpr double kDeadSlotCost = 0.25, kRecordCost = 0.1;
+// relative costs in units of one live 4 KiB block, fitted
+// to forced dense / 8-block layouts of uniform 7..26-block objects with the
+// dense launches' nt sc1 stores (profiles/r02/diag/batch_lab_store_cost.log)
+constexpr double kDeadSlotCost = 0.4, kRecordCost = 0.05;
 constexpr int kPrepParts = 4;                   // host threads per sub-batch pass
 constexpr uint64_t kPrepMinPerPart = 8192;      // descriptors below which a pass stays single-threaded
 
