@@ -99,7 +99,8 @@ int s3dg_set_stream_tiles(s3dg_ctx *ctx, int on);
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident
  * workgroups per CU cap (0 = none), draws per lane (>= 64; sets lanes per
  * chunk; launches too small to fill the GPU use shorter spans, down to 256), store cache policy (as s3dg_set_store_policy, negative =
- * default).  0 = default for each (both modes: 64, 4, 1024 draws, sc1).
+ * default).  0 = default for each (both modes: 64, 4, 1024 draws, sc1; DG1
+ * with a zero prefix: 512 draws).
  * A tuning knob; results are identical. */
 int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int wgs_per_cu,
                              uint64_t min_lane_draws, int store_policy);

@@ -42,6 +42,10 @@ constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
 constexpr int kDefaultStoreDense = kStoreNTSC1;
 constexpr uint64_t kDefaultKsMinDraws[2] = {1024, 1024};   // npz keystream, DG1
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
+// DG1 with a zero prefix (compress > 1): 512 draws per lane by default, so the
+// waves that skip the PRNG cover more of each block's prefix (d1 c2: 6413 ->
+// 6694 GB/s; at c1 the extra jumps cost: 5896 -> 5347, profiles/r02/diag/k2_xcd.log)
+constexpr uint64_t kDgenPrefixMinDraws = 512;
 // measured on MI355X (tools/k2_lab.py, profiles/r02/diag/k2_lab_r2e.log):
 // 512-B row pieces, 4-wave workgroups, 1024 draws per lane and sc1 stores for
 // both modes (K2 6010 vs 5803 GB/s at 2048 draws; DG1 c1 5933 / c2 6158 vs
@@ -833,12 +837,13 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
 }
 
 // lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
-static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t nchunks, KeystreamArgs &A,
-                          const uint64_t **jtab) {
+static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t nchunks, bool zero_prefix,
+                          KeystreamArgs &A, const uint64_t **jtab) {
     const uint64_t nd = chunk_bytes / 8;
     // as many lanes per chunk as keep >= ks_min_draws draws per lane (the
     // jump costs 256 steps); up to 1024 lanes = 16 waves per chunk
-    const uint64_t min_draws = c->ks_min_draws[mode];
+    uint64_t min_draws = c->ks_min_draws[mode];
+    if (mode == 1 && zero_prefix && min_draws == kDefaultKsMinDraws[1]) min_draws = kDgenPrefixMinDraws;
     uint32_t lpc = 1;
     while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
     // small launches (a few chunks): spread each chunk over more lanes, down
@@ -878,7 +883,7 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
     if (!dst || !aligned16(dst)) return fail(S3DG_EINVAL, "dst must be a 16-byte aligned device pointer");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, 0, chunk_bytes, (len + chunk_bytes - 1) / chunk_bytes, A, &jt)) return r;
+    if (int r = keystream_plan(c, 0, chunk_bytes, (len + chunk_bytes - 1) / chunk_bytes, false, A, &jt)) return r;
     A.nchunks = (len + chunk_bytes - 1) / chunk_bytes;
     A.chunk_bytes = chunk_bytes;
     A.obj_len = len;
@@ -920,7 +925,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, 1, kDgenBlock, (blk_hi - blk_lo) * n_objs, A, &jt)) return r;
+    if (int r = keystream_plan(c, 1, kDgenBlock, (blk_hi - blk_lo) * n_objs, f_num > 0, A, &jt)) return r;
     const uint64_t U = s3dg_unique_blocks(nb, dedup);
     A.cpo = blk_hi - blk_lo;
     A.nchunks = A.cpo * n_objs;

@@ -23,7 +23,9 @@
 #include "s3dg_internal.h"
 
 // Diagnostic builds only (tools/ablate.py): bit 0 = no window patch phase,
-// bit 1 = no PRNG chain.  Outputs of such builds are wrong by design.
+// bit 1 = no PRNG chain; k_keystream: bit 5 = no Xoshiro steps in the draw
+// loop (counter draws), bit 6 = no jump-ahead.  Outputs of such builds are
+// wrong by design.
 #ifndef S3DG_ABLATE
 #define S3DG_ABLATE 0
 #endif
@@ -584,6 +586,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         return;
     }
 
+#if !(S3DG_ABLATE & 64)
     if (lpc > 1 && sub > 0) {                    // jump to draw sub*span
         // state <- sum over set bits i of J of step^i(state): 256 steps, the
         // polynomial read as 8 32-bit halves so each step's mask is one
@@ -602,6 +605,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         }
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     }
+#endif
     row_dest();
 
     // Wave-uniform fast paths: a D-draw group needs no masking when no lane
@@ -619,8 +623,12 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         if (__all(it >= it_plain && it != it_tail)) {
 #pragma unroll
             for (int q = 0; q < D; q += 2) {
+#if S3DG_ABLATE & 32
+                const uint64_t ra = s0 + q, rbv = s3 + q;
+#else
                 const uint64_t ra = xo_out(s0, s3); xo_step(s0, s1, s2, s3);
                 const uint64_t rbv = xo_out(s0, s3); xo_step(s0, s1, s2, s3);
+#endif
                 *reinterpret_cast<u32x4 *>(myrows + l * RS + q * 8) =
                     u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
             }

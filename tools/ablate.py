@@ -6,7 +6,7 @@ import ctypes, json, os, statistics, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
-VARIANTS = ["0", "1", "2", "3"]     # S3DG_ABLATE bits: 1 = no window patch, 2 = no PRNG chain
+VARIANTS = os.environ.get("ABLATE_VARIANTS", "0,1,2,3").split(",")   # S3DG_ABLATE bits (s3dg_kernels.hip)
 
 
 def build():

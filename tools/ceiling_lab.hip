@@ -294,3 +294,49 @@ extern "C" __attribute__((visibility("default"))) int lab_v11x(void *dst, uint64
     }
     return (int)hipGetLastError();
 }
+
+// V13: K2's store shape with XCD-aware region ownership.  Regions are `R`
+// bytes; workgroups are dealt round-robin to the 8 XCDs, so workgroup b
+// (XCD b mod 8) takes regions = b (mod 8) only: region (b>>3)*256*8 + 8*lw + (b&7)
+// for its 256 lanes lw.  Each lane writes its region in `seg`-byte stages, rows
+// as K2 (seg/16 lanes per row).  xcd=0: the same stages, wave-contiguous regions (V11).
+// Policy: 0 plain, 2 sc1, 3 nt sc1.
+template <int POL>
+__device__ __forceinline__ void stp(uint8_t *p, u32x4 v) {
+    if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else *(u32x4 *)p = v;
+}
+template <int SEG, int POL>
+__global__ __launch_bounds__(256) void v13_xcd(uint8_t *dst, uint64_t nreg, uint32_t R, int xcd, uint32_t pat) {
+    const u32x4 v = {pat, pat + 1, pat + 2, pat + 3};
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t b = blockIdx.x;
+    constexpr uint32_t lpr = SEG / 16, rpi = 64 / lpr;
+    // region of row `row` of this wave
+    auto region = [&](uint32_t row) -> uint64_t {
+        const uint32_t lw = w * 64 + row;
+        return xcd ? (b >> 3) * 2048 + 8ull * lw + (b & 7) : b * 256 + lw;
+    };
+    for (uint32_t it = 0; it < R / SEG; ++it)
+#pragma unroll
+        for (uint32_t i = 0; i < lpr; ++i) {
+            const uint32_t row = i * rpi + l / lpr;
+            const uint64_t rg = region(row);
+            if (rg < nreg) stp<POL>(dst + rg * R + it * SEG + (l % lpr) * 16, v);
+        }
+}
+extern "C" __attribute__((visibility("default"))) int lab_v13(void *dst, uint64_t len, uint32_t R, int seg, int xcd,
+                                                              int pol, void *s) {
+    const uint64_t nreg = len / R;
+    const dim3 g((uint32_t)((nreg + 2047) / 2048 * 8));
+#define V13(SG, P) hipLaunchKernelGGL((v13_xcd<SG, P>), g, dim3(256), 0, (hipStream_t)s, (uint8_t *)dst, nreg, R, xcd, 7u)
+    if (seg == 512 && pol == 0) V13(512, 0);
+    else if (seg == 512 && pol == 2) V13(512, 2);
+    else if (seg == 512 && pol == 3) V13(512, 3);
+    else if (seg == 1024 && pol == 2) V13(1024, 2);
+    else if (seg == 256 && pol == 2) V13(256, 2);
+    else return -1;
+#undef V13
+    return (int)hipGetLastError();
+}

@@ -58,6 +58,17 @@ def main():
                         lambda g=seg, t=nt, d=lds: L.lab_v11x(ctypes.c_void_p(p), ctypes.c_uint64(n), 32768, g, t, d,
                                                             ctypes.c_void_p(sh)))
         V["v10 ceiling 2D nx=2048"] = lambda: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), 2048, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh))
+    if "--xcd" in sys.argv:   # K2 store shape, XCD-aware region ownership vs wave-contiguous
+        V.clear()
+        L.lab_v13.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_void_p]
+        for R, seg, pol in [(4096, 512, 2), (4096, 512, 0), (4096, 512, 3), (8192, 512, 2), (4096, 1024, 2),
+                            (4096, 256, 2), (16384, 512, 2)]:
+            for x in (0, 1):
+                V[f"v13 region={R} seg={seg} pol={pol} xcd={x}"] = (
+                    lambda r=R, g=seg, q=pol, xx=x: L.lab_v13(ctypes.c_void_p(p), ctypes.c_uint64(n), r, g, xx, q,
+                                                             ctypes.c_void_p(sh)))
+        V["v10 ceiling 2D nx=2048"] = lambda: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), 2048, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh))
     V["torch fill_"] = lambda: buf.fill_(7)
     res = {k: [] for k in V}
     for _ in range(5):
