@@ -21,7 +21,8 @@ SOURCES = [os.path.join(CSRC, "s3dg_kernels.hip"), os.path.join(CSRC, "s3dg_capi
            os.path.join(CSRC, "s3dg_jump.cpp"), os.path.join(CSRC, "s3dg_generator.cpp"),
            os.path.join(CSRC, "s3dg_crc.hip"), os.path.join(CSRC, "s3dg_npz.cpp"),
            os.path.join(CSRC, "s3dg_object.cpp"), os.path.join(CSRC, "s3dg_put.cpp"),
-           os.path.join(CSRC, "s3dg_numa.cpp"), os.path.join(CSRC, "s3dg_host.cpp")]
+           os.path.join(CSRC, "s3dg_numa.cpp"), os.path.join(CSRC, "s3dg_host.cpp"),
+           os.path.join(CSRC, "s3dg_batch.hip")]
 HEADERS = [os.path.join(CSRC, "s3dg_internal.h"), os.path.join(CSRC, "s3dg_jump.h"),
            os.path.join(ROOT, "include", "s3dlio_gpu.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

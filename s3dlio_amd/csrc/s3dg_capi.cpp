@@ -72,7 +72,10 @@ struct StreamState {
     int bnext = 0;
     hipStream_t up = nullptr;          // batch entry uploads + record maps (overlap the previous fill)
     struct Stage {
-        BatchEnt *host = nullptr, *dev = nullptr;   // pinned staging / device copy
+        s3dg_obj_desc *host = nullptr, *dev = nullptr;   // pinned staging / device copy
+        uint64_t *rec_lo = nullptr;    // device: record offset of each object (tile layouts)
+        void *scan_tmp = nullptr;      // device: scan scratch
+        size_t scan_tmp_bytes = 0;
         uint64_t cap = 0;
         hipEvent_t uploaded = nullptr;  // host staging may be rewritten
         hipEvent_t consumed = nullptr;  // device copy may be freed (k_batch_map done; both on `up`)
@@ -287,7 +290,8 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
         }
         for (auto &G : S->stage) {
             if (G.host) (void)hipHostFree(G.host);
-            if (G.dev) (void)hipFree(G.dev);
+            for (void *p : {(void *)G.dev, (void *)G.rec_lo, G.scan_tmp})
+                if (p) (void)hipFree(p);
             if (G.uploaded) (void)hipEventDestroy(G.uploaded);
             if (G.consumed) (void)hipEventDestroy(G.consumed);
         }
@@ -560,11 +564,13 @@ int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {
 }
 
 // Mixed-size batch ("Batches"): the descriptors are cut into
-// sub-batches (16 Ki objects first, doubling to 256 Ki) so the host's two
-// passes over sub-batch k+1 overlap the GPU's fill of sub-batch k.  Per
-// sub-batch the host only validates, counts slots and writes 64-B BatchEnts
-// into pinned staging; the upload runs on the stream's side stream, and
-// k_batch_map derives prefix parameters and tile records on the device.
+// sub-batches (16 Ki objects first, doubling to 256 Ki) so the host's pass
+// over sub-batch k+1 overlaps the GPU's fill of sub-batch k.  Per sub-batch
+// the host makes one pass on up to 8 threads: it validates, counts slots and
+// copies the 40-B descriptors into pinned staging (empty ones squeezed out
+// afterwards); the upload runs on the stream's side
+// stream, where a device scan of the tile counts gives each object's record
+// offset and k_batch_map derives prefix parameters and tile records.
 // Record layout per sub-batch (cost model below):
 //   * tiles of 2^tshift blocks (8..64) per object, the object's block 0 at
 //     slot `lead` = its 4 KiB granule (mod 8): XCD-aligned, dead slots at
@@ -579,7 +585,7 @@ constexpr uint64_t kBatchSubFirst = 16384, kBatchSubMax = 262144;
 // to forced dense / 8-block layouts of uniform 7..26-block objects with the
 // dense launches' nt sc1 stores (profiles/r02/diag/batch_lab_store_cost.log)
 constexpr double kDeadSlotCost = 0.4, kRecordCost = 0.05;
-constexpr int kPrepParts = 4;                   // host threads per sub-batch pass
+constexpr int kPrepParts = 8;                   // host threads per sub-batch pass
 constexpr uint64_t kPrepMinPerPart = 8192;      // descriptors below which a pass stays single-threaded
 
 // A few persistent host threads for the batch passes: run(parts, fn) calls
@@ -651,9 +657,11 @@ struct BatchScan {
     const char *msg = nullptr;
 };
 
-static void batch_scan(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P) {
+static void batch_scan(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P,
+                       s3dg_obj_desc *out) {
     for (uint64_t k = k0; k < k1; ++k) {
-        const s3dg_obj_desc &o = d[k];
+        const s3dg_obj_desc o = d[k];
+        out[k - k0] = o;   // staged as is; empty objects are squeezed out afterwards (rare)
         if (o.size == 0) continue;
         if (o.dst_off & 15u) { P.err = S3DG_EINVAL; P.msg = "dst_off must be a multiple of 16"; return; }
         if (o.f_den == 0 || o.f_num >= o.f_den) { P.err = S3DG_EINVAL; P.msg = "need f_num < f_den"; return; }
@@ -671,40 +679,6 @@ static void batch_scan(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr
     }
 }
 
-// Pass 2: entries j0.. of [k0, k1) with their record ranges, records from rec0
-// (tile layouts) or per granule from lead0 + (dst_off - first_off) / 4 KiB (dense).
-// In the dense layout an entry's rec_hi is the next object's first granule;
-// the caller patches the last entry of every part.
-static void batch_write(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr_t base, uint32_t tshift,
-                        uint64_t lead0, uint64_t first_off, uint64_t j0, uint64_t rec0, BatchEnt *out) {
-    uint64_t rec = rec0, j = j0;
-    for (uint64_t k = k0; k < k1; ++k) {
-        const s3dg_obj_desc &o = d[k];
-        if (o.size == 0) continue;
-        const uint64_t nb = (o.size + kBlk - 1) / kBlk;
-        BatchEnt &e = out[j];
-        e.dst_off = o.dst_off;
-        e.size = o.size;
-        e.entropy = o.entropy;
-        e.dedup = o.dedup;
-        e.f_num = o.f_num;
-        e.f_den = o.f_den;
-        if (tshift == 0) {
-            const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
-            e.blk0 = g0;
-            e.rec_lo = j == 0 ? 0 : g0;
-            if (j > j0) out[j - 1].rec_hi = g0;   // the gap before this object: dead records
-            e.rec_hi = g0 + nb;
-        } else {
-            const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
-            e.rec_lo = rec;
-            rec += (nb + lead + (1ull << tshift) - 1) >> tshift;
-            e.rec_hi = rec;
-            e.blk0 = (e.rec_lo << tshift) + lead;
-        }
-        ++j;
-    }
-}
 
 int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc *d, uint64_t n,
                                void *stream) {
@@ -729,13 +703,38 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     for (uint64_t k0 = 0; k0 < n;) {
         const uint64_t k1 = n - k0 < sub ? n : k0 + sub;
         sub = sub * 2 < kBatchSubMax ? sub * 2 : kBatchSubMax;
-        // pass 1 in parts, then merged in order
+        // staging: host buffer free once its last upload finished, device copy
+        // once the k_batch_map that read it finished
+        StreamState::Stage &G = S->stage[S->next];
+        S->next ^= 1;
+        HIP_TRY(hipEventSynchronize(G.uploaded), "hipEventSynchronize(batch staging)");
+        if (k1 - k0 > G.cap) {
+            HIP_TRY(hipEventSynchronize(G.consumed), "hipEventSynchronize(batch staging)");
+            if (G.host) (void)hipHostFree(G.host);
+            for (void *p : {(void *)G.dev, (void *)G.rec_lo, G.scan_tmp})
+                if (p) (void)hipFree(p);
+            G.host = nullptr; G.dev = nullptr; G.rec_lo = nullptr; G.scan_tmp = nullptr;
+            G.cap = 0; G.scan_tmp_bytes = 0;
+            const uint64_t cap = k1 - k0 < 1024 ? 1024 : k1 - k0;
+            size_t tmp = 0;
+            HIP_TRY(launch_batch_scan(nullptr, cap, kTileShiftMin, 0, nullptr, nullptr, &tmp, S->up),
+                    "hipcub scan size");
+            HIP_TRY(hipHostMalloc((void **)&G.host, cap * sizeof(s3dg_obj_desc), hipHostMallocDefault),
+                    "hipHostMalloc(batch staging)");
+            HIP_TRY(hipMalloc((void **)&G.dev, cap * sizeof(s3dg_obj_desc)), "hipMalloc(batch staging)");
+            HIP_TRY(hipMalloc((void **)&G.rec_lo, cap * sizeof(uint64_t)), "hipMalloc(batch records)");
+            HIP_TRY(hipMalloc(&G.scan_tmp, tmp ? tmp : 1), "hipMalloc(batch scan)");
+            G.scan_tmp_bytes = tmp;
+            G.cap = cap;
+        }
+        s3dg_obj_desc *H = G.host;
+        // one pass in parts (validate, count, stage), then merged in order
         int parts = (int)((k1 - k0) / kPrepMinPerPart);
         parts = parts < 1 ? 1 : (parts > kPrepParts ? kPrepParts : parts);
         uint64_t cut[kPrepParts + 1];
         for (int q = 0; q <= parts; ++q) cut[q] = k0 + (k1 - k0) * (uint64_t)q / (uint64_t)parts;
         BatchScan part[kPrepParts];
-        pool.run(parts, [&](int q) { batch_scan(d, cut[q], cut[q + 1], base, part[q]); });
+        pool.run(parts, [&](int q) { batch_scan(d, cut[q], cut[q + 1], base, part[q], H + (cut[q] - k0)); });
         BatchScan P;
         for (int q = 0; q < parts; ++q) {
             const BatchScan &Q = part[q];
@@ -767,36 +766,12 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             if (P.dense_ok && kDeadSlotCost * (double)(span - P.blocks) + kRecordCost * (double)span < best)
                 tshift = 0;
         }
-        // staging: host buffer free once its last upload finished, device copy
-        // once the k_batch_map that read it finished
-        StreamState::Stage &G = S->stage[S->next];
-        S->next ^= 1;
-        HIP_TRY(hipEventSynchronize(G.uploaded), "hipEventSynchronize(batch staging)");
-        if (m > G.cap) {
-            HIP_TRY(hipEventSynchronize(G.consumed), "hipEventSynchronize(batch staging)");
-            if (G.host) (void)hipHostFree(G.host);
-            if (G.dev) (void)hipFree(G.dev);
-            G.host = nullptr; G.dev = nullptr; G.cap = 0;
-            const uint64_t cap = m < 1024 ? 1024 : m;
-            HIP_TRY(hipHostMalloc((void **)&G.host, cap * sizeof(BatchEnt), hipHostMallocDefault),
-                    "hipHostMalloc(batch staging)");
-            HIP_TRY(hipMalloc((void **)&G.dev, cap * sizeof(BatchEnt)), "hipMalloc(batch staging)");
-            G.cap = cap;
+        if (m != k1 - k0) {   // squeeze out the empty objects
+            uint64_t j = 0;
+            for (uint64_t i = 0; i < k1 - k0; ++i)
+                if (H[i].size) H[j++] = H[i];
         }
-        // pass 2 in the same parts: entry and record offsets from the part counts
-        uint64_t j0[kPrepParts], rec0[kPrepParts];
-        for (int q = 0; q < parts; ++q) {
-            j0[q] = q ? j0[q - 1] + part[q - 1].m : 0;
-            rec0[q] = q ? rec0[q - 1] + (tshift ? part[q - 1].ntiles[tshift] : 0) : 0;
-        }
-        BatchEnt *H = G.host;
-        pool.run(parts, [&](int q) {
-            batch_write(d, cut[q], cut[q + 1], base, tshift, lead0, P.first_off, j0[q], rec0[q], H);
-        });
-        if (tshift == 0)     // a part's last object ends where the next part's first begins
-            for (int q = 1; q < parts; ++q)
-                if (part[q].m && j0[q]) H[j0[q] - 1].rec_hi = H[j0[q]].blk0;
-        const uint64_t recs = tshift == 0 ? span : rec0[parts - 1] + part[parts - 1].ntiles[tshift];
+        const uint64_t recs = tshift == 0 ? span : P.ntiles[tshift];
         // record map tb: free once the fill two sub-batches back has read it
         const int tb = S->bnext;
         S->bnext ^= 1;
@@ -810,11 +785,16 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             S->btile_cap[tb] = cap;
         }
         // upload and map on the side stream, overlapping the previous fill
-        HIP_TRY(hipMemcpyAsync(G.dev, G.host, m * sizeof(BatchEnt), hipMemcpyHostToDevice, S->up),
-                "hipMemcpyAsync(batch entries)");
+        HIP_TRY(hipMemcpyAsync(G.dev, G.host, m * sizeof(s3dg_obj_desc), hipMemcpyHostToDevice, S->up),
+                "hipMemcpyAsync(batch descriptors)");
         HIP_TRY(hipEventRecord(G.uploaded, S->up), "hipEventRecord");
+        if (tshift) {
+            size_t tmp = G.scan_tmp_bytes;
+            HIP_TRY(launch_batch_scan(G.dev, m, tshift, base, G.rec_lo, G.scan_tmp, &tmp, S->up), "hipcub scan");
+        }
         HIP_TRY(hipStreamWaitEvent(S->up, S->filled[tb], 0), "hipStreamWaitEvent");
-        HIP_TRY(launch_batch_map(G.dev, m, S->btiles[tb], tshift, S->up), "launch k_batch_map");
+        HIP_TRY(launch_batch_map(G.dev, m, G.rec_lo, S->btiles[tb], tshift, base, lead0, P.first_off, S->up),
+                "launch k_batch_map");
         HIP_TRY(hipEventRecord(G.consumed, S->up), "hipEventRecord");
         HIP_TRY(hipEventRecord(S->mapped[tb], S->up), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(s, S->mapped[tb], 0), "hipStreamWaitEvent");

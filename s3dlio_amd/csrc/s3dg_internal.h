@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
+#include "s3dlio_gpu.h"
+
 extern "C" int s3dg_internal_fail(int code, const char *msg);
 struct s3dg_ctx;
 
@@ -36,20 +38,12 @@ struct PrefixParams {
 // Kurz 2019, "Faster remainder by direct computation"); exact for all a, d < 2^32.
 inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
 
-// Batch entry as uploaded (64 B): the caller's descriptor plus its record
-// range.  Records [rec_lo, rec_hi) of the launch belong to this object; its
-// block 0 sits at slot blk0 (slot = record << tshift + position in the tile).
-// k_batch_map derives the prefix parameters on the device.
-struct BatchEnt {
-    uint64_t dst_off;
-    uint64_t size;
-    uint64_t entropy;
-    uint64_t dedup;
-    uint64_t rec_lo, rec_hi;
-    uint64_t blk0;
-    uint32_t f_num, f_den;
-};
-static_assert(sizeof(BatchEnt) == 64, "BatchEnt is 64 bytes");
+// Batch sub-batches reach the device as the caller's 40-B descriptors
+// (empty objects dropped); the record ranges are derived there:
+// tile layouts by an exclusive scan of the objects' tile counts
+// (launch_batch_scan, s3dg_batch.hip), the dense layout from each object's
+// granule and its successor's (k_batch_map).
+static_assert(sizeof(s3dg_obj_desc) == 40, "s3dg_obj_desc is 40 bytes");
 
 // One tile (2^tshift slots) of a batch object, written by k_batch_map /
 // k_tile_map_uniform so the fill
@@ -86,10 +80,19 @@ hipError_t launch_fill_stream(const LaunchCfg &lc, uint8_t *dst, uint64_t obj_si
                               uint32_t blk_hi, uint64_t seed_base, uint64_t first_obj,
                               PrefixParams pp, const void *base_dev, hipStream_t s);
 
-// Batch records built on the device from uploaded BatchEnts (k_batch_map:
-// prefix parameters per object, then its records), then k_fill_batch over
-// total_recs << tshift slots.
-hipError_t launch_batch_map(const BatchEnt *ents, uint64_t n, TileRec *tiles, uint32_t tshift, hipStream_t s);
+// Batch records built on the device from the uploaded descriptors (the scan,
+// then k_batch_map: prefix parameters per object and its records), then
+// k_fill_batch over total_recs << tshift slots.
+// Sub-batch records from its n non-empty descriptors d (device): tile
+// layouts (tshift >= kTileShiftMin) read rec_lo[k] = the exclusive scan of
+// the tile counts; the dense layout (tshift 0) places object k's block 0 at
+// slot lead0 + (d[k].dst_off - first_off) / 4 KiB.
+hipError_t launch_batch_map(const s3dg_obj_desc *d, uint64_t n, const uint64_t *rec_lo, TileRec *tiles,
+                            uint32_t tshift, uintptr_t base, uint64_t lead0, uint64_t first_off, hipStream_t s);
+// rec_lo[k] = sum of tiles(d[j]) for j < k, tiles(o) = (blocks + lead + 2^tshift - 1) >> tshift,
+// lead = ((base + o.dst_off) >> 12) & 7.  tmp == nullptr: *tmp_bytes = the scratch size n needs.
+hipError_t launch_batch_scan(const s3dg_obj_desc *d, uint64_t n, uint32_t tshift, uintptr_t base, uint64_t *rec_lo,
+                             void *tmp, size_t *tmp_bytes, hipStream_t s);
 hipError_t launch_batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t total_tiles, uint32_t tshift,
                               TileRec *tiles, const void *base_dev, hipStream_t s);
 

@@ -394,22 +394,38 @@ __device__ PrefixParams dev_make_prefix(uint64_t nb, uint64_t dedup, uint32_t f_
     return pp;
 }
 
-// Records of a batch launch from its uploaded entries, one thread per object:
-// record q in [rec_lo, rec_hi) maps slot (q << tshift) + k to block
-// (q - rec_lo) << tshift + k - lead, lead = blk0 - (rec_lo << tshift).
-__global__ __launch_bounds__(256) void k_batch_map(const BatchEnt *ents, uint64_t n, TileRec *tiles,
-                                                   uint32_t tshift) {
+// Records of a batch sub-batch from its uploaded descriptors, one thread per
+// object: record q in [rec_lo, rec_hi) maps slot (q << tshift) + k to block
+// (q - rec_lo) << tshift + k - lead.  Tile layouts: rec_lo from the scan, lead
+// = the object's granule mod 8 (XCD alignment).  Dense: rec_lo = the object's
+// granule slot (0 for the first object, whose lead is lead0), rec_hi = the
+// next object's, so the gap records before it are its dead slots.
+__global__ __launch_bounds__(256) void k_batch_map(const s3dg_obj_desc *d, uint64_t n, const uint64_t *scan,
+                                                   TileRec *tiles, uint32_t tshift, uint64_t base, uint64_t lead0,
+                                                   uint64_t first_off) {
     const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
-    const BatchEnt e = ents[k];
+    const s3dg_obj_desc o = d[k];
+    const uint64_t nb = (o.size + kBlk - 1) / kBlk;
+    uint64_t rec_lo, rec_hi, lead;
+    if (tshift == 0) {
+        const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
+        rec_lo = k == 0 ? 0 : g0;
+        rec_hi = k + 1 < n ? lead0 + (d[k + 1].dst_off - first_off) / kBlk : g0 + nb;
+        lead = g0 - rec_lo;
+    } else {
+        lead = ((base + o.dst_off) >> 12) & 7;
+        rec_lo = scan[k];
+        rec_hi = rec_lo + ((nb + lead + (1ull << tshift) - 1) >> tshift);
+    }
     TileRec r;
-    r.dst_off = e.dst_off;
-    r.size = e.size;
-    r.entropy = e.entropy;
-    r.lead = (uint32_t)(e.blk0 - (e.rec_lo << tshift));
-    r.pp = dev_make_prefix((e.size + kBlk - 1) / kBlk, e.dedup, e.f_num, e.f_den);
-    for (uint64_t q = e.rec_lo; q < e.rec_hi; ++q) {
-        r.first = (uint32_t)((q - e.rec_lo) << tshift);
+    r.dst_off = o.dst_off;
+    r.size = o.size;
+    r.entropy = o.entropy;
+    r.lead = (uint32_t)lead;
+    r.pp = dev_make_prefix(nb, o.dedup, o.f_num, o.f_den);
+    for (uint64_t q = rec_lo; q < rec_hi; ++q) {
+        r.first = (uint32_t)((q - rec_lo) << tshift);
         tiles[q] = r;
     }
 }
@@ -854,10 +870,12 @@ hipError_t launch_batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t t
     return batch_tiles(lc, dst_base, total_tiles, tshift, tiles, base_dev, s, false);
 }
 
-hipError_t launch_batch_map(const BatchEnt *ents, uint64_t n, TileRec *tiles, uint32_t tshift, hipStream_t s) {
+hipError_t launch_batch_map(const s3dg_obj_desc *d, uint64_t n, const uint64_t *rec_lo, TileRec *tiles,
+                            uint32_t tshift, uintptr_t base, uint64_t lead0, uint64_t first_off, hipStream_t s) {
     (void)hipGetLastError();
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_batch_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, ents, n, tiles, tshift);
+    hipLaunchKernelGGL(k_batch_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d, n, rec_lo, tiles, tshift,
+                       (uint64_t)base, lead0, first_off);
     return hipGetLastError();
 }
 
