@@ -84,7 +84,7 @@ int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_c
  * the L2 with later tile records; 0 = off, UINT32_MAX = default (256).
  * Results are identical. */
 int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
-/* Batch launches: blocks per tile record (8, 16, 32 or 64), 1 = dense (one
+/* Batch launches: blocks per tile record (2, 4, 8, 16, 32 or 64), 1 = dense (one
  * record per 4 KiB granule of the batch's address range; used only when
  * the objects are 4 KiB-aligned, sorted and non-overlapping); 0 = chosen per
  * sub-batch by cost (default).  Results are identical. */

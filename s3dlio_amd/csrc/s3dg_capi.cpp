@@ -183,7 +183,7 @@ constexpr uint64_t kTileCost = 2;
 uint32_t pick_tile_shift(const uint64_t (&ntiles)[kTileShiftMax + 1]) {
     uint32_t best = kTileShiftMax;
     uint64_t best_cost = UINT64_MAX;
-    for (uint32_t sh = kTileShiftMax; sh >= kTileShiftMin; --sh) {
+    for (uint32_t sh = kTileShiftMax; sh >= kTileShiftAutoMin; --sh) {
         const uint64_t cost = (ntiles[sh] << sh) + kTileCost * ntiles[sh];
         if (cost < best_cost) { best_cost = cost; best = sh; }
     }
@@ -379,7 +379,7 @@ int s3dg_set_batch_tile(s3dg_ctx *c, uint32_t blocks) {
     if (blocks > 1) {
         while ((1u << sh) < blocks) ++sh;
         if ((1u << sh) != blocks || sh < kTileShiftMin || sh > kTileShiftMax)
-            return fail(S3DG_EINVAL, "tile blocks must be 0 (per launch), 1 (dense), 8, 16, 32 or 64");
+            return fail(S3DG_EINVAL, "tile blocks must be 0 (per launch), 1 (dense), 2, 4, 8, 16, 32 or 64");
     }
     c->tile_shift = sh;
     c->tile_force_dense = blocks == 1;
@@ -572,7 +572,7 @@ int s3dg_set_stream_tiles(s3dg_ctx *c, int on) {
 // stream, where a device scan of the tile counts gives each object's record
 // offset and k_batch_map derives prefix parameters and tile records.
 // Record layout per sub-batch (cost model below):
-//   * tiles of 2^tshift blocks (8..64) per object, the object's block 0 at
+//   * tiles of 2^tshift blocks (2..64) per object, the object's block 0 at
 //     slot `lead` = its 4 KiB granule (mod 8): XCD-aligned, dead slots at
 //     both ends of every object;
 //   * dense (tshift 0): objects 4 KiB-aligned, sorted and non-overlapping;
@@ -758,7 +758,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         else if (c->tile_shift) tshift = c->tile_shift;
         else {
             double best = 1e300;
-            for (uint32_t sh = kTileShiftMax; sh >= kTileShiftMin; --sh) {
+            for (uint32_t sh = kTileShiftMax; sh >= kTileShiftAutoMin; --sh) {
                 const double cost =
                     kDeadSlotCost * (double)((P.ntiles[sh] << sh) - P.blocks) + kRecordCost * (double)P.ntiles[sh];
                 if (cost < best) { best = cost; tshift = sh; }

@@ -17,7 +17,11 @@ constexpr uint32_t kMod = 32;     // MOD_SIZE   src/constants.rs:352
 constexpr uint64_t kDgenBlock = 1ull << 20;   // DGEN_BLOCK_SIZE src/constants.rs:348
 // batch tiles (tile -> object map granule) are 2^tshift blocks, tshift in
 // [kTileShiftMin, kTileShiftMax], chosen per launch (s3dg_capi.cpp pick_tile_shift)
-constexpr uint32_t kTileShiftMin = 3, kTileShiftMax = 6;
+constexpr uint32_t kTileShiftMin = 1, kTileShiftMax = 6;
+// the per-launch choice considers 8..64-block tiles only: 2- and 4-block tiles
+// (s3dg_set_batch_tile) cut dead slots but lose more to records, e.g. 16-B
+// packed 20 KiB objects 2556 vs 2917 GB/s (profiles/r02/diag/desc40/ab3_*.log)
+constexpr uint32_t kTileShiftAutoMin = 3;
 // tshift 0 (one record per 4 KiB granule of the batch's address range, no
 // per-object lead) is the dense layout for small packed objects
 constexpr int kWavesPerWG = 4;

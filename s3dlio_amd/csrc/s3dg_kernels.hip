@@ -310,7 +310,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 // start (lead) or past its end exit.  lead makes g = 4 KiB-granule address
 // (mod 8), as in the stream kernel: workgroups are dealt round-robin to the
 // 8 XCDs, so XCD x writes only granules = x (mod 8).
-// Tiles are 2^tshift blocks (8..64, chosen per launch by the host so the
+// Tiles are 2^tshift blocks (2..64, chosen per launch by the host so the
 // dead workgroups of ragged object tails stay few).
 // pf > 0: the first 8 workgroups of every 256 blocks (one per XCD: workgroups
 // are dealt round-robin to the XCDs) touch the records of the 256 blocks

@@ -46,7 +46,7 @@ def _knobs(ctx, rnd):
     sp = rnd.choice([-1, 0, 1, 2, 3])
     ctx.set_store_policy(sp, sp)
     ctx.set_batch_prefetch(rnd.choice([-1, 0, 1, 7, 128, 256, 1 << 20]))
-    ctx.set_batch_tile(rnd.choice([0, 0, 8, 16, 32, 64]))
+    ctx.set_batch_tile(rnd.choice([0, 0, 1, 2, 4, 8, 16, 32, 64]))
 
 
 def _reset(ctx):

@@ -215,7 +215,8 @@ def test_tile_map_shared_across_streams(gpu_ctx, torch, oracle, base):
 
 @pytest.mark.parametrize("waves,occ,pf,sp,tile", [
     (1, -1, 128, -1, 0), (2, -1, 128, 0, 64), (4, -1, 128, 1, 8), (1, 0, 0, 0, 16), (1, 20, 1, 1, 32),
-    (2, 12, 3, 2, 8), (1, -1, 100000, -1, 64), (2, 14, 64, 3, 0), (1, -1, 128, -1, 8), (1, 26, 0, -1, 16)])
+    (2, 12, 3, 2, 8), (1, -1, 100000, -1, 64), (2, 14, 64, 3, 0), (1, -1, 128, -1, 8), (1, 26, 0, -1, 16),
+    (1, -1, 256, -1, 2), (2, -1, 256, 3, 4)])
 def test_batch_mixed_sizes_vs_oracle(gpu_ctx, torch, oracle, base, waves, occ, pf, sp, tile):
     gpu_ctx.set_waves_per_block(waves)
     gpu_ctx.set_occupancy(occ, occ)
@@ -380,7 +381,7 @@ def test_invalid_arguments_raise(gpu_ctx, torch):
         gpu_ctx.fill_controlled(int(t.data_ptr()) + 1, 100)
     with pytest.raises(ValueError):
         gpu_ctx.fill_stream(t, obj_size=4096, n_objs=2, stride=100)
-    for bad in (2, 4, 9, 128):
+    for bad in (3, 9, 128):
         with pytest.raises(ValueError, match="tile"):
             gpu_ctx.set_batch_tile(bad)
 
