@@ -193,7 +193,7 @@ def main() -> int:
         return launch_ranks(args.gpus)
     import torch
     from s3dlio_amd import Context, compress_ratio, object_entropy
-    from s3dlio_amd._lib import ObjDesc, call
+    from s3dlio_amd._lib import ObjDesc, call, lib
     from s3dlio_amd.shard import ControlPlane, object_range
 
     cp = ControlPlane()
@@ -277,8 +277,21 @@ def main() -> int:
         ring = torch.empty(size, dtype=torch.uint8, device=f"cuda:{dev}")
         base_ptr = int(ring.data_ptr())
         calls = args.objects or cfg["n"]
+        # the calls come from a native loop (tools/native_loop.c), as the
+        # reference's criterion loop calls from Rust; the Python-loop rate is
+        # reported beside it (single_call)
+        nl = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libnative_loop.so"))
+        u64, u32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p
+        nl.nl_fill_loop.restype = ctypes.c_int
+        nl.nl_fill_loop.argtypes = [vp, vp, vp, u64, u64, u64, u32, u32, u64, vp]
+        fill_ptr = ctypes.cast(lib.s3dg_fill_controlled, vp)
 
         def single_step(size=size, calls=calls):
+            r = nl.nl_fill_loop(fill_ptr, ctx._h, base_ptr, size, calls, d, fn, fd, 7, sh)
+            if r:
+                raise RuntimeError(f"s3dg_fill_controlled failed in the native loop ({r})")
+
+        def single_step_py(size=size, calls=calls):
             for _ in range(calls):
                 call("s3dg_fill_controlled", ctx._h, base_ptr, size, d, fn, fd, 7, sh)
         launches.append((single_step, calls * size))
@@ -351,6 +364,18 @@ def main() -> int:
     total_bytes = cp.sum(step_bytes) * args.steps
     value = total_bytes / elapsed / GiB
 
+    single_call = None
+    if kind == "single":   # the same calls from a Python loop (ctypes), once, for comparison
+        single_step_py()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream); single_step_py(); e1.record(stream); torch.cuda.synchronize()
+        py_s = e0.elapsed_time(e1) * 1e-3
+        single_call = {"caller": "native loop (tools/native_loop.c) over the C ABI",
+                       "us_per_call": round(avg_ms * 1e3, 3),
+                       "python_loop_us_per_call": round(py_s / calls * 1e6, 3),
+                       "python_loop_GBps": round(calls * cfg["size"] / py_s / 1e9, 1)}
+
     # ---- verification: sampled objects of the last writes vs the C oracle ---------------
     verified = None
     if not args.no_verify:
@@ -410,13 +435,16 @@ def main() -> int:
                        else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
                        "stores": (args.store if args.store != "default"
-                                  else {"keystream": "sc1", "dgen": "sc1"}.get(kind, "sc1" if kind == "batch"
-                                                                                  or tiled else "nt sc1"))},
+                                  else {"keystream": "sc1", "dgen": "sc1",
+                                        "batch": "sc1 (tiled layouts), nt sc1 (dense layout)"}.get(
+                                      kind, "sc1" if tiled else "nt sc1"))},
             "roofline": roof,
             "cpu_baseline": cpu,
             "d2h_inclusive": d2h,
             "verified_vs_oracle": verified,
         }
+        if single_call:
+            out["single_call"] = single_call
         print(json.dumps(out), flush=True)
     cp.close()
     return 0

@@ -58,8 +58,27 @@ def build_bytesview(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+NL_SRC = os.path.join(ROOT, "tools", "native_loop.c")
+NL_LIB = os.path.join(ROOT, "tools", "_build", "libnative_loop.so")
+
+
+def build_native_loop(force: bool = False, verbose: bool = False) -> str:
+    """bench.py's native call loop (tools/native_loop.c; not part of the library)."""
+    if not os.path.exists(NL_SRC):
+        return ""
+    if not force and os.path.exists(NL_LIB) and os.path.getmtime(NL_LIB) >= os.path.getmtime(NL_SRC):
+        return NL_LIB
+    os.makedirs(os.path.dirname(NL_LIB), exist_ok=True)
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Werror", "-o", NL_LIB, NL_SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return NL_LIB
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     build_bytesview(force, verbose)
+    build_native_loop(force, verbose)
     if not force and not _stale():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",

@@ -37,7 +37,8 @@ def main():
     from s3dlio_amd._lib import ObjDesc, call
     MiB = 1 << 20
     n = int(os.environ.get("LAB_N", "10000"))
-    ctx = Context(0)
+    bs = os.environ.get("LAB_BASE_SEED")      # e.g. bench.py's 0xBA5EB10C00000000
+    ctx = Context(0, base_seed=int(bs, 0)) if bs else Context(0)
     pts = list(points())
 
     def table(sizes, d, fn, fd, align=4096):
