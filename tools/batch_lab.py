@@ -63,8 +63,9 @@ def main():
         sz, d, fn, fd, *al = (int(x) for x in k[1:].split("x"))
         al = al[0] if al else 4096
         descs[k] = table([sz] * min(5 * n * MiB // sz, 52 * 10**9 // ((sz + al - 1) // al * al)), d, fn, fd, al)
-    # generic uniform streams: "s<size>x<dedup>x<f_num>x<f_den>[x<align>]" (k_fill_stream)
-    for k in {p[0] for p in pts if p[0].startswith("s") and p[0][1:2].isdigit()}:
+    # generic uniform streams: "s<size>x<dedup>x<f_num>x<f_den>[x<align>]" (k_fill_stream);
+    # "t<size>x..." the same through the tiled path (s3dg_set_stream_tiles 1, as bench.py)
+    for k in {p[0] for p in pts if p[0][:1] in ("s", "t") and p[0][1:2].isdigit()}:
         sz, d, fn, fd, *al = (int(x) for x in k[1:].split("x"))
         al = al[0] if al else 4096
         stride = (sz + al - 1) // al * al
@@ -107,7 +108,7 @@ def main():
             ctx.set_occupancy(o, o)
             ctx.set_batch_prefetch(f)
             ctx.set_batch_tile(p[5])
-            ctx.set_stream_tiles(1 if k in ("stream2t", "stream3t", "stream5t") else 0)
+            ctx.set_stream_tiles(1 if k in ("stream2t", "stream3t", "stream5t") or k[:1] == "t" else 0)
             occ[p] = ctx.query_occupancy(batch=not k.startswith(("stream", "ceiling")) and not k[1:2].isdigit()
                                          or k.startswith("u"))
             run(k)
