@@ -657,28 +657,44 @@ struct BatchScan {
     const char *msg = nullptr;
 };
 
-static void batch_scan(const s3dg_obj_desc *d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P,
-                       s3dg_obj_desc *out) {
+static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P,
+                       s3dg_obj_desc *__restrict out) {
+    // accumulators in registers (P aliases nothing, but the compiler cannot
+    // know that across the staging stores); the checks fold into one flag
+    uint64_t m = 0, blocks = 0, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
+    bool dense = true, bad = false;
     for (uint64_t k = k0; k < k1; ++k) {
         const s3dg_obj_desc o = d[k];
         out[k - k0] = o;   // staged as is; empty objects are squeezed out afterwards (rare)
         if (o.size == 0) continue;
-        if (o.dst_off & 15u) { P.err = S3DG_EINVAL; P.msg = "dst_off must be a multiple of 16"; return; }
-        if (o.f_den == 0 || o.f_num >= o.f_den) { P.err = S3DG_EINVAL; P.msg = "need f_num < f_den"; return; }
         const uint64_t nb = (o.size + kBlk - 1) / kBlk;
-        if (nb >= (1ull << 31)) { P.err = S3DG_EINVAL; P.msg = "object larger than 2^31 blocks"; return; }
-        const uint64_t lead = ((base + o.dst_off) >> 12) & 7;
-        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh)
-            P.ntiles[sh] += (nb + lead + (1ull << sh) - 1) >> sh;
-        if (P.m == 0) P.first_off = o.dst_off;
-        else if (o.dst_off < P.last_end) P.dense_ok = false;
-        if (o.dst_off & (kBlk - 1)) P.dense_ok = false;
-        P.last_end = o.dst_off + nb * kBlk;
-        P.blocks += nb;
-        ++P.m;
+        bad |= (o.dst_off & 15u) != 0 || o.f_den == 0 || o.f_num >= o.f_den || nb >= (1ull << 31);
+        const uint64_t x = nb + (((base + o.dst_off) >> 12) & 7);   // blocks behind the XCD lead
+        for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) nt[sh] += (x + (1ull << sh) - 1) >> sh;
+        if (m == 0) first = o.dst_off;
+        dense = dense && (m == 0 || o.dst_off >= last) && (o.dst_off & (kBlk - 1)) == 0;
+        last = o.dst_off + nb * kBlk;
+        blocks += nb;
+        ++m;
     }
+    if (bad) {   // the first offending descriptor names the error
+        for (uint64_t k = k0; k < k1; ++k) {
+            const s3dg_obj_desc &o = d[k];
+            if (o.size == 0) continue;
+            P.err = S3DG_EINVAL;
+            if (o.dst_off & 15u) { P.msg = "dst_off must be a multiple of 16"; return; }
+            if (o.f_den == 0 || o.f_num >= o.f_den) { P.msg = "need f_num < f_den"; return; }
+            if ((o.size + kBlk - 1) / kBlk >= (1ull << 31)) { P.msg = "object larger than 2^31 blocks"; return; }
+            P.err = S3DG_OK;
+        }
+    }
+    P.m = m;
+    P.blocks = blocks;
+    P.first_off = first;
+    P.last_end = last;
+    P.dense_ok = dense;
+    for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles[sh] = nt[sh];
 }
-
 
 int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc *d, uint64_t n,
                                void *stream) {
