@@ -69,6 +69,11 @@ def main():
                     lambda r=R, g=seg, q=pol, xx=x: L.lab_v13(ctypes.c_void_p(p), ctypes.c_uint64(n), r, g, xx, q,
                                                              ctypes.c_void_p(sh)))
         V["v10 ceiling 2D nx=2048"] = lambda: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), 2048, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh))
+    if "--k2stride" in sys.argv:   # K2 store shape at non-power-of-two region strides (seg 512)
+        V.clear()
+        for R in (8192, 8704, 9216, 12288, 16384, 16896, 32768, 33280, 5120, 4608):
+            V[f"v11 region={R} seg=512"] = (lambda r=R: L.lab_v11(ctypes.c_void_p(p), ctypes.c_uint64(n // r * r // 64 * 64 if False else n), r, 512, ctypes.c_void_p(sh)))
+        V["v10 ceiling 2D nx=2048"] = lambda: L.lab_v9(ctypes.c_void_p(p), ctypes.c_uint64(n), 2048, 1, ctypes.c_void_p(bp), ctypes.c_void_p(sh))
     V["torch fill_"] = lambda: buf.fill_(7)
     res = {k: [] for k in V}
     for _ in range(5):
