@@ -29,9 +29,23 @@
 #ifndef S3DG_ABLATE
 #define S3DG_ABLATE 0
 #endif
+// Diagnostic builds only: S3DG_KS_TRACE = per-wave wall-clock stamps of
+// k_keystream; S3DG_KS_JUMP bit 0 = per-lane vector jump even when the wave's
+// lanes share a chunk (A/B; outputs identical).
+#ifndef S3DG_KS_TRACE
+#define S3DG_KS_TRACE 0
+#endif
+#ifndef S3DG_KS_JUMP
+#define S3DG_KS_JUMP 0
+#endif
 
 
 namespace s3dg {
+#if S3DG_KS_TRACE
+// Diagnostic builds only: per-wave start/end wall-clock stamps of k_keystream
+// (tools/ks_trace_lab.py).
+__device__ uint64_t *g_ks_trace;
+#endif
 namespace {
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -527,6 +541,9 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     constexpr int P = D / 2;           // 16-byte pieces per row
     constexpr int R = 64 / P;          // rows per store instruction
     __shared__ __attribute__((aligned(16))) uint8_t rows[W][64 * RS];
+#if S3DG_KS_TRACE
+    const uint64_t t_start = wall_clock64();
+#endif
     const uint32_t t = threadIdx.x, l = t & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     uint8_t *myrows = rows[w];
@@ -603,7 +620,30 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     }
 
 #if !(S3DG_ABLATE & 64)
-    if (lpc > 1 && sub > 0) {                    // jump to draw sub*span
+    if (lpc >= 64 && !(S3DG_KS_JUMP & 1)) {
+        // Every lane of the wave is in one chunk, so the sequence step^i(s)
+        // is wave-uniform: it runs on the scalar unit (64-bit s_xor/s_lshl,
+        // SGPRs) and each lane only accumulates the states its own jump
+        // polynomial selects (8 v_bitop3 with an SGPR operand per step, was
+        // 8 + the 11-op vector step).  Lane sub = 0 has J = 1: a = s.
+        uint64_t u0 = readlane64(s0, 0), u1 = readlane64(s1, 0);
+        uint64_t u2 = readlane64(s2, 0), u3 = readlane64(s3, 0);
+        const uint32_t *J = reinterpret_cast<const uint32_t *>(jtab + 4 * sub);
+        uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        for (int h = 0; h < 8; ++h) {
+            const uint32_t jw = J[h];
+#pragma unroll 8
+            for (int b = 0; b < 32; ++b) {
+                const uint32_t m = (uint32_t)((int32_t)(jw << (31 - b)) >> 31);
+                a0 = and_xor_64(u0, a0, m); a1 = and_xor_64(u1, a1, m);
+                a2 = and_xor_64(u2, a2, m); a3 = and_xor_64(u3, a3, m);
+                const uint64_t t = u1 << 17;    // reference step order, scalar
+                u2 ^= u0; u3 ^= u1; u1 ^= u2; u0 ^= u3; u2 ^= t;
+                u3 = rotl64(u3, 45);
+            }
+        }
+        s0 = a0; s1 = a1; s2 = a2; s3 = a3;
+    } else if (lpc > 1 && sub > 0) {             // jump to draw sub*span
         // state <- sum over set bits i of J of step^i(state): 256 steps, the
         // polynomial read as 8 32-bit halves so each step's mask is one
         // sign-extended bit field and each accumulate one v_bitop3
@@ -706,6 +746,13 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+#if S3DG_KS_TRACE
+    if (l == 0 && g_ks_trace) {
+        const uint64_t wi = (uint64_t)blockIdx.x * W + w;
+        g_ks_trace[2 * wi] = t_start;
+        g_ks_trace[2 * wi + 1] = wall_clock64();
+    }
+#endif
 }
 
 template <int D, int W>
@@ -938,3 +985,9 @@ hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len,
 }
 
 }  // namespace s3dg
+
+#if S3DG_KS_TRACE
+extern "C" int s3dg_diag_ks_trace(void *buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(s3dg::g_ks_trace), &buf, sizeof(buf));
+}
+#endif

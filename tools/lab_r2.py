@@ -79,10 +79,28 @@ def main():
     W["dg1c1"] = (lambda: call("s3dg_dgen_fill", ctx._h, base, dn, 0, 1 << 40, 1, 0, 1, 12345, sh), dn, 1)
     W["dg1c2"] = (lambda: call("s3dg_dgen_fill", ctx._h, base, dn, 0, 1 << 40, 2, 1, 2, 12345, sh), dn, 1)
     W["k2"] = (lambda: call("s3dg_xoshiro_fill", ctx._h, base, dn, 2 * MiB, 0, sh), dn, 1)
+    # launch size: the same bytes as 8 GiB launches (bench configs 14/15) or one launch
+    nbig = cap // (8 * GiB)
+    for nm, d_, fn_, fd_ in (("dg1c1", 1, 0, 1), ("dg1c2", 2, 1, 2)):
+        W[nm + "_8g"] = (lambda d_=d_, fn_=fn_, fd_=fd_: [call("s3dg_dgen_fill", ctx._h, base + t * 8 * GiB, 8 * GiB,
+                                                               0, 1 << 40, d_, fn_, fd_, 12345 + t, sh)
+                                                          for t in range(nbig)], nbig * 8 * GiB, 1)
+        W[nm + "_all"] = (lambda d_=d_, fn_=fn_, fd_=fd_: call("s3dg_dgen_fill", ctx._h, base, nbig * 8 * GiB, 0,
+                                                               1 << 40, d_, fn_, fd_, 12345, sh), nbig * 8 * GiB, 1)
+    W["k2_8g"] = (lambda: [call("s3dg_xoshiro_fill", ctx._h, base + t * 8 * GiB, 8 * GiB, 2 * MiB, t * 4096, sh)
+                           for t in range(nbig)], nbig * 8 * GiB, 1)
+    W["k2_all"] = (lambda: call("s3dg_xoshiro_fill", ctx._h, base, nbig * 8 * GiB, 2 * MiB, 0, sh),
+                   nbig * 8 * GiB, 1)
     # the reference's criterion shape (benches/performance_microbenchmarks.rs:43-64): one
     # fill_controlled_data call on one buffer, back to back
     for nm, sz in (("one1m", MiB), ("one4m", 4 * MiB), ("one16m", 16 * MiB)):
         W[nm] = (lambda sz=sz: call("s3dg_fill_controlled", ctx._h, base, sz, 1, 0, 1, 7, sh), sz, 200)
+
+    # the floor of a back-to-back 1 MiB launch: a store-only kernel and hipMemsetD32Async
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemsetD32Async.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+    W["memset1m"] = (lambda: hip.hipMemsetD32Async(base, 0x5A5A5A5A, MiB // 4, sh), MiB, 200)
+    W["ceil1m"] = (lambda: call("s3dg_write_ceiling", ctx._h, base, MiB, 0xA5A5A5A5, sh), MiB, 200)
 
     # "<kind>@<tile>": the same workload with s3dg_set_batch_tile(tile) (1 = dense)
     for k in list(kinds):

@@ -74,7 +74,8 @@ def main():
             off += (sz + 4095) // 4096 * 4096
         descs[kind] = (arr, sum(sizes), off)
     crcs = {}
-    work = {"stream2": 8 * MiB * n, "k2": 8 * MiB * n, "stream3": 8 * MiB * n, "stream5": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
+    work = {"stream2": 8 * MiB * n, "k2": 8 * MiB * n, "k2_8g": 8 * MiB * n, "dg1": 8 * MiB * n,
+            "dg1_8g": 8 * MiB * n, "dg1c2_8g": 8 * MiB * n, "stream3": 8 * MiB * n, "stream5": 8 * MiB * n, "ceiling": 8 * MiB * n, "crc": 8 * MiB * n,
             **{k: v[1] for k, v in descs.items()}}
     buf = torch.empty(max([8 * MiB * n] + [v[2] for v in descs.values()]), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
@@ -88,6 +89,17 @@ def main():
                                               u64(SEED_BASE), u64(0), sh)
         elif kind == "k2":                   # xoshiro keystream, 2 MiB chunks
             r = L.s3dg_xoshiro_fill(h, p, u64(8 * MiB * n), u64(2 * MiB), u64(0), sh)
+        elif kind in ("k2_8g", "dg1", "dg1_8g", "dg1c2_8g"):   # keystream / DG1 launches of 8 GiB or one
+            per = 8 << 30 if kind.endswith("_8g") else 8 * MiB * n
+            r = 0
+            for t in range((8 * MiB * n) // per):
+                q = ctypes.c_void_p(buf.data_ptr() + t * per)
+                if kind == "k2_8g":
+                    r |= L.s3dg_xoshiro_fill(h, q, u64(per), u64(2 * MiB), u64(t * (per // (2 * MiB))), sh)
+                else:
+                    d, fn, fd = (2, 1, 2) if kind == "dg1c2_8g" else (1, 0, 1)
+                    r |= L.s3dg_dgen_fill(h, q, u64(per), u64(0), u64(1 << 40), u64(d), u32(fn), u32(fd),
+                                          u64(777 + t), sh)
         elif kind == "ceiling":
             r = L.s3dg_write_ceiling(h, p, u64(8 * MiB * n), u32(0xA5A5A5A5), sh)
         elif kind == "crc":                  # synchronous: device regions + host fold
@@ -111,8 +123,10 @@ def main():
                 assert L.s3dg_set_batch_prefetch(h, u32(f)) == 0
                 assert L.s3dg_set_store_policy(h, sp, sp) == 0
                 assert L.s3dg_set_batch_tile(h, u32(tb)) == 0
-                if k == "k2":                  # k2: waves, wgs/CU, min lane draws, store
+                if k.startswith("k2"):         # k2 / dg1: waves, wgs/CU, min lane draws, store
                     assert L.s3dg_set_keystream_shape(h, 0, 64, w, o, u64(f), sp) == 0
+                if k.startswith("dg1"):
+                    assert L.s3dg_set_keystream_shape(h, 1, 64, w, o, u64(f), sp) == 0
                 run(L, h, k)
                 torch.cuda.synchronize()
                 if k == "crc":
