@@ -17,7 +17,8 @@ the batch API, 8/9 config 1's 64 KiB objects on the GPU (stream / batch API),
 10 small ragged objects through the batch API, 11-13 one
 s3dg_fill_controlled call on a single 1/4/16 MiB buffer (the reference's own
 criterion shape, benches/performance_microbenchmarks.rs:43-64), 14/15 the
-DG1 byte path behind generate_data / Generator.
+DG1 byte path behind generate_data / Generator (one launch per object), 16/17
+the same objects through s3dg_dgen_fill_stream (one launch per step).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 `roofline` (kernel-event timing vs the 8 TB/s HBM peak, and vs the fill's own
@@ -76,6 +77,10 @@ CONFIGS = {
              n=10, size=8 * GiB, dedup=1, compress=1, scaling="weak"),
     15: dict(name="dg1: 10 x 8 GiB DG1 objects (generate_data byte path), dedup=2 compress=2", kind="dgen",
              n=10, size=8 * GiB, dedup=2, compress=2, scaling="weak"),
+    16: dict(name="dg1 stream: 10 x 8 GiB DG1 objects in one s3dg_dgen_fill_stream launch, dedup=1 compress=1",
+             kind="dgen_stream", n=10, size=8 * GiB, dedup=1, compress=1, scaling="weak"),
+    17: dict(name="dg1 stream: 10 x 8 GiB DG1 objects in one s3dg_dgen_fill_stream launch, dedup=2 compress=2",
+             kind="dgen_stream", n=10, size=8 * GiB, dedup=2, compress=2, scaling="weak"),
 }
 
 
@@ -297,6 +302,17 @@ def main() -> int:
         launches.append((single_step, calls * size))
         samples = [(0, ("single", size))]
         step_bytes = calls * size
+    elif kind == "dgen_stream":   # DG1 objects, one launch per ring pass
+        size = cfg["size"]
+        ring_objs = max(1, min(n_rank, ring_cap // size))
+        ring = torch.empty(ring_objs * size, dtype=torch.uint8, device=f"cuda:{dev}")
+        base_ptr = int(ring.data_ptr())
+        for s0 in range(0, n_rank, ring_objs):
+            k = min(ring_objs, n_rank - s0)
+            launches.append((lambda k=k, first=lo + s0: call("s3dg_dgen_fill_stream", ctx._h, base_ptr, size, size,
+                                                             k, d, fn, fd, SEED_BASE, first, sh), k * size))
+            samples = [(t * size, ("dgen", lo + s0 + t)) for t in range(k)]
+        step_bytes = n_rank * size
     else:   # dgen
         size = cfg["size"]
         ring_objs = max(1, min(n_rank, ring_cap // size))
@@ -315,11 +331,15 @@ def main() -> int:
              and all(b // cfg["size"] * ((cfg["size"] + 4095) // 4096) >= 16384 for _, b in launches)
              and cfg["size"] % (32 * KiB) == 0)
     if kind == "keystream":
-        kernel, launch_shape = "k_keystream", ("k_keystream<64,4>: 256 lanes x 1024 draws per 2 MiB chunk "
-                                               "(jump-ahead), 64-draw LDS stage per lane, 512-B row pieces per store")
-    elif kind == "dgen":
-        kernel, launch_shape = "k_keystream (DG1 mode)", ("k_keystream<64,4>: 1024 draws per lane, 128 lanes per "
-                                                          "1 MiB DG1 block, zero-prefix waves skip the PRNG")
+        kernel, launch_shape = "k_keystream", ("k_keystream<64,4>: 64 lanes x 4096 draws per 2 MiB chunk "
+                                               "(jump-ahead, state sequence on the scalar unit), 64-draw LDS stage "
+                                               "per lane, 512-B row pieces per store")
+    elif kind in ("dgen", "dgen_stream"):
+        kernel, launch_shape = "k_keystream (DG1 mode)", (
+            "k_keystream<64,4>: " + ("512 draws per lane, 256 lanes per 1 MiB DG1 block, zero-prefix waves skip "
+                                     "the PRNG" if fn else "2048 draws per lane, 64 lanes per 1 MiB DG1 block, "
+                                     "jump state sequence on the scalar unit")
+            + ("; all objects of the step in one launch" if kind == "dgen_stream" else "; one launch per object"))
     else:
         batch = kind == "batch" or tiled
         kernel = ("k_fill_batch" + (" (uniform tile records)" if tiled else "")) if batch else "k_fill_stream"
@@ -392,7 +412,7 @@ def main() -> int:
 
     # ---- D2H-inclusive rate (bounded sample; never `value`) -------------------------------
     d2h = None
-    if not args.no_d2h and kind in ("stream", "keystream", "dgen"):
+    if not args.no_d2h and kind in ("stream", "keystream", "dgen", "dgen_stream"):
         reps = [d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo) for _ in range(max(1, args.d2h_reps))]
         d2h = reps[-1]
         if len(reps) > 1:
@@ -435,7 +455,7 @@ def main() -> int:
                        else cfg["compress"],
                        "launches_per_step": len(launches), "parallelism": f"object-stream x{world}",
                        "stores": (args.store if args.store != "default"
-                                  else {"keystream": "sc1", "dgen": "sc1",
+                                  else {"keystream": "sc1", "dgen": "sc1", "dgen_stream": "sc1",
                                         "batch": "sc1 (tiled layouts), nt sc1 (dense layout)"}.get(
                                       kind, "sc1" if tiled else "nt sc1"))},
             "roofline": roof,
@@ -571,8 +591,9 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
     the copy stream), so run-to-run spread can be attributed."""
     kind = cfg["kind"]
     size = cfg["size"]
-    per_chunk = max(1, chunk // size) if kind != "dgen" else 1
-    cb = per_chunk * size if kind != "dgen" else chunk
+    dg = kind in ("dgen", "dgen_stream")
+    per_chunk = max(1, chunk // size) if not dg else 1
+    cb = per_chunk * size if not dg else chunk
     nchunks = total // cb
     gen = torch.cuda.Stream(device=dev)
     cpy = torch.cuda.Stream(device=dev)
@@ -595,7 +616,7 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
             if kind == "keystream":
                 call("s3dg_xoshiro_fill", ctx._h, int(devbuf[s].data_ptr()), cb, 2 * MiB,
                      (lo * size + k * cb) // (2 * MiB), int(gen.cuda_stream))
-            elif kind == "dgen":
+            elif kind in ("dgen", "dgen_stream"):
                 call("s3dg_dgen_fill", ctx._h, int(devbuf[s].data_ptr()), size, k * (cb >> 20),
                      (k + 1) * (cb >> 20), cfg["dedup"], fn, fd, SEED_BASE, int(gen.cuda_stream))
             else:

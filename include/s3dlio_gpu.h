@@ -99,8 +99,9 @@ int s3dg_set_stream_tiles(s3dg_ctx *ctx, int on);
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident
  * workgroups per CU cap (0 = none), draws per lane (>= 64; sets lanes per
  * chunk; launches too small to fill the GPU use shorter spans, down to 256), store cache policy (as s3dg_set_store_policy, negative =
- * default).  0 = default for each (both modes: 64, 4, 1024 draws, sc1; DG1
- * with a zero prefix: 512 draws).
+ * default).  0 = default for each (both modes: 64, 4, 2048 draws, sc1; K2
+ * launches of >= 8 rounds of resident waves: 4096 draws; DG1 with a zero
+ * prefix: 512 draws).
  * A tuning knob; results are identical. */
 int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int wgs_per_cu,
                              uint64_t min_lane_draws, int store_policy);
@@ -157,6 +158,13 @@ int s3dg_xoshiro_fill(s3dg_ctx *ctx, void *dst, uint64_t len, uint64_t chunk_byt
 int s3dg_dgen_fill(s3dg_ctx *ctx, void *dst, uint64_t obj_size, uint64_t blk_lo,
                    uint64_t blk_hi, uint64_t dedup, uint32_t f_num, uint32_t f_den,
                    uint64_t seed, void *stream);
+/* n_objs DG1 objects of obj_size bytes in one launch: object j at
+ * dst + j*stride, seeded s3dg_object_entropy(seed_base, first_obj + j), i.e.
+ * the bytes of n_objs s3dg_dgen_fill calls (ObjectGen / DataGenerator fanned
+ * out over many objects).  stride >= obj_size, 16-byte aligned. */
+int s3dg_dgen_fill_stream(s3dg_ctx *ctx, void *dst, uint64_t obj_size, uint64_t stride,
+                          uint64_t n_objs, uint64_t dedup, uint32_t f_num, uint32_t f_den,
+                          uint64_t seed_base, uint64_t first_obj, void *stream);
 /* Host helper: advance a Xoshiro256 state by n steps with the jump polynomial
  * the kernels use (test/diagnostic; no GPU needed). */
 int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n);

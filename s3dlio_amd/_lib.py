@@ -79,6 +79,7 @@ SIGNATURES = {
     "s3dg_xoshiro_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_vp]),
     "s3dg_xoshiro_jump": (c_int, [ctypes.POINTER(c_u64), c_u64]),
     "s3dg_dgen_fill": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32, c_u64, c_vp]),
+    "s3dg_dgen_fill_stream": (c_int, [c_vp, c_vp, c_u64, c_u64, c_u64, c_u64, c_u32, c_u32, c_u64, c_u64, c_vp]),
     "s3dg_gen_create": (c_int, [c_u64, c_u64, c_u64, c_int, c_u64, ctypes.POINTER(c_vp)]),
     "s3dg_gen_create_ratio": (c_int, [c_u64, c_u64, c_u32, c_u32, c_int, c_u64,
                                       ctypes.POINTER(c_vp)]),

@@ -40,7 +40,16 @@ constexpr int kDefaultStoreStream = kStoreNTSC1, kDefaultStoreBatch = kStoreSC1;
 // (tools/batch_lab.py, profiles/r02/diag/batch_lab_store_*: 20 KiB+5 objects 4766 -> 6092 GB/s,
 // dense 32 KiB 5977 -> 6663, dense 64 KiB 5992 -> 6472; tiled layouts keep sc1)
 constexpr int kDefaultStoreDense = kStoreNTSC1;
-constexpr uint64_t kDefaultKsMinDraws[2] = {1024, 1024};   // npz keystream, DG1
+// Draws per lane (npz keystream, DG1).  Since the jump's state sequence runs
+// on the scalar unit (k_keystream), longer lanes win: 2048 draws per lane
+// (K2 8 GiB launches 6096 -> 6621 GB/s, 80 GiB 6436 -> 6596; DG1 c1 6141 ->
+// 6604 / 6434 -> 6621; profiles/r02/diag/ks/ks_draws_sweep.log), and K2
+// launches of at least kKsLongRounds rounds of resident waves take 4096
+// (80 GiB: 6718; 8 GiB, 4 rounds: 6437, so not there).  DG1 stays at 2048:
+// at 4096 a wave would span two 1 MiB blocks and lose the scalar jump.
+constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 2048};
+constexpr uint64_t kKsLongDraws = 4096;
+constexpr uint64_t kKsLongRounds = 8;
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
 // DG1 with a zero prefix (compress > 1): 512 draws per lane by default, so the
 // waves that skip the PRNG cover more of each block's prefix (d1 c2: 6413 ->
@@ -840,6 +849,12 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     // jump costs 256 steps); up to 1024 lanes = 16 waves per chunk
     uint64_t min_draws = c->ks_min_draws[mode];
     if (mode == 1 && zero_prefix && min_draws == kDefaultKsMinDraws[1]) min_draws = kDgenPrefixMinDraws;
+    if (mode == 0 && min_draws == kDefaultKsMinDraws[0] && nd >= 64 * kKsLongDraws) {
+        // waves at 4096 draws per lane vs the chip's resident keystream waves
+        // (one 4-wave workgroup per CU at the default shape)
+        const uint64_t waves = nchunks * (nd / kKsLongDraws) / 64;
+        if (waves >= kKsLongRounds * (uint64_t)c->cus * (uint64_t)c->ks[0].waves) min_draws = kKsLongDraws;
+    }
     uint32_t lpc = 1;
     while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
     // small launches (a few chunks): spread each chunk over more lanes, down
@@ -902,6 +917,14 @@ int s3dg_dgen_fill(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t blk_lo, u
                    uint64_t dedup, uint32_t f_num, uint32_t f_den, uint64_t seed, void *stream) {
     return s3dg_internal_dgen_chunk(c, dst, obj_size, 0, 1, blk_lo, blk_hi, dedup, f_num, f_den, seed, 0,
                                     stream);
+}
+
+int s3dg_dgen_fill_stream(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t stride, uint64_t n_objs,
+                          uint64_t dedup, uint32_t f_num, uint32_t f_den, uint64_t seed_base,
+                          uint64_t first_obj, void *stream) {
+    if (n_objs > 1 && stride < obj_size) return fail(S3DG_EINVAL, "stride < obj_size: objects overlap");
+    return s3dg_internal_dgen_chunk(c, dst, obj_size, stride, n_objs, 0, ~0ull, dedup, f_num, f_den, seed_base,
+                                    first_obj, stream);
 }
 
 // n_objs equal DG1 objects in one launch: blocks [blk_lo, blk_hi) of object

@@ -281,6 +281,17 @@ class Context:
         call("s3dg_dgen_fill", self._h, self._dst(dst, need), int(obj_size), int(blk_lo), int(hi),
              int(dedup), fn, fd, int(seed) & (2**64 - 1), self._s(stream))
 
+    def dgen_fill_stream(self, dst, obj_size: int, n_objs: int, stride: int | None = None,
+                         dedup: int = 1, compress=1, seed_base: int = 0, first_obj: int = 0,
+                         stream=None) -> None:
+        """n_objs DG1 objects in one launch, object j at dst + j*stride seeded
+        object_entropy(seed_base, first_obj + j): the bytes of n_objs dgen_fill calls."""
+        stride = obj_size if stride is None else stride
+        need = (int(n_objs) - 1) * int(stride) + int(obj_size) if n_objs > 0 and obj_size > 0 else 0
+        fn, fd = compress_ratio(compress)
+        call("s3dg_dgen_fill_stream", self._h, self._dst(dst, need), int(obj_size), int(stride), int(n_objs),
+             int(dedup), fn, fd, int(seed_base) & (2**64 - 1), int(first_obj), self._s(stream))
+
     def write_ceiling(self, dst, nbytes: int | None = None, pattern: int = 0xA5A5A5A5,
                       stream=None) -> None:
         n = _nbytes(dst) if nbytes is None else int(nbytes)

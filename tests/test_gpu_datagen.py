@@ -54,6 +54,39 @@ def test_device_dgen_fill_ranges(S, oracle, gpu_ctx):
     assert bytes(full[:size].cpu().numpy()) == bytes(oracle.dgen_fill(size, 2, 2, 3, 5))
 
 
+@pytest.mark.parametrize("size,stride,n,d,c", [
+    (3 * MiB + 5, 4 * MiB, 5, 2, 3), (MiB, MiB, 7, 1, 1), (2 * MiB, 2 * MiB, 3, 1, 2), (4096 + 16, 8192, 9, 1, 1),
+    (40 * MiB, 40 * MiB, 2, 4, 2),
+])
+def test_device_dgen_fill_stream_equals_per_object(S, oracle, gpu_ctx, size, stride, n, d, c):
+    """s3dg_dgen_fill_stream: n objects in one launch = n s3dg_dgen_fill calls
+    seeded object_entropy(seed_base, first_obj + j), every byte, guard bytes kept."""
+    import torch
+    seed_base, first = 0x5EED000000000001, 11
+    buf = torch.full(((n - 1) * stride + size + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    gpu_ctx.dgen_fill_stream(buf, size, n, stride=stride, dedup=d, compress=c, seed_base=seed_base,
+                             first_obj=first)
+    ref = torch.full_like(buf, 0xAB)
+    for j in range(n):
+        gpu_ctx.dgen_fill(ref[j * stride:], size, dedup=d, compress=c,
+                          seed=S.object_entropy(seed_base, first + j))
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    fn, fd = S.compress_ratio(c)
+    got = buf.cpu().numpy()
+    for j in (0, n - 1):
+        exp = oracle.dgen_fill(size, d, fn, fd, S.object_entropy(seed_base, first + j))
+        assert bytes(got[j * stride:j * stride + size]) == bytes(exp)
+    assert (got[(n - 1) * stride + size:] == 0xAB).all()
+
+
+def test_device_dgen_fill_stream_rejects_overlap(S, gpu_ctx):
+    import torch
+    buf = torch.empty(8 * MiB, dtype=torch.uint8, device="cuda")
+    with pytest.raises(Exception):
+        gpu_ctx.dgen_fill_stream(buf, 2 * MiB, 2, stride=MiB)
+
+
 @pytest.mark.parametrize("size", [1, 2, 7, 1023, 1024, 1025, 4096, MiB - 1, MiB, MiB + 1])
 def test_exact_sizes(S, size):
     """tests/test_data-gen.rs:24-39, tests/test_comprehensive_streaming.rs:39-51."""
