@@ -628,8 +628,13 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         // 8 + the 11-op vector step).  Lane sub = 0 has J = 1: a = s.
         uint64_t u0 = readlane64(s0, 0), u1 = readlane64(s1, 0);
         uint64_t u2 = readlane64(s2, 0), u3 = readlane64(s3, 0);
-        const uint32_t *J = reinterpret_cast<const uint32_t *>(jtab + 4 * sub);
+        // the lane's 256-bit polynomial in two loads up front (one load and
+        // wait per 32 steps before)
+        const uint4 *Jv = reinterpret_cast<const uint4 *>(jtab + 4 * sub);
+        const uint4 j0 = Jv[0], j1 = Jv[1];
+        const uint32_t J[8] = {j0.x, j0.y, j0.z, j0.w, j1.x, j1.y, j1.z, j1.w};
         uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
         for (int h = 0; h < 8; ++h) {
             const uint32_t jw = J[h];
 #pragma unroll 8
