@@ -331,14 +331,16 @@ def main() -> int:
              and all(b // cfg["size"] * ((cfg["size"] + 4095) // 4096) >= 16384 for _, b in launches)
              and cfg["size"] % (32 * KiB) == 0)
     if kind == "keystream":
-        kernel, launch_shape = "k_keystream", ("k_keystream<64,4>: 64 lanes x 4096 draws per 2 MiB chunk "
+        kernel, launch_shape = "k_keystream", ("k_keystream<64,1>: 64 lanes x 4096 draws per 2 MiB chunk "
                                                "(jump-ahead, state sequence on the scalar unit), 64-draw LDS stage "
-                                               "per lane, 512-B row pieces per store")
+                                               "per lane, 512-B row pieces per store, 1-wave workgroups in XCD "
+                                               "groups of 16")
     elif kind in ("dgen", "dgen_stream"):
         kernel, launch_shape = "k_keystream (DG1 mode)", (
-            "k_keystream<64,4>: " + ("512 draws per lane, 256 lanes per 1 MiB DG1 block, zero-prefix waves skip "
-                                     "the PRNG" if fn else "2048 draws per lane, 64 lanes per 1 MiB DG1 block, "
-                                     "jump state sequence on the scalar unit")
+            ("k_keystream<64,4>: 512 draws per lane, 256 lanes per 1 MiB DG1 block, zero-prefix waves skip "
+             "the PRNG, XCD groups of 32 waves" if fn else
+             "k_keystream<64,1>: 2048 draws per lane, 64 lanes per 1 MiB DG1 block, jump state sequence on the "
+             "scalar unit, XCD groups of 16 waves")
             + ("; all objects of the step in one launch" if kind == "dgen_stream" else "; one launch per object"))
     else:
         batch = kind == "batch" or tiled

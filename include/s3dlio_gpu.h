@@ -99,12 +99,18 @@ int s3dg_set_stream_tiles(s3dg_ctx *ctx, int on);
  * per store round (16, 32 or 64), waves per workgroup (1, 2 or 4), resident
  * workgroups per CU cap (0 = none), draws per lane (>= 64; sets lanes per
  * chunk; launches too small to fill the GPU use shorter spans, down to 256), store cache policy (as s3dg_set_store_policy, negative =
- * default).  0 = default for each (both modes: 64, 4, 2048 draws, sc1; K2
+ * default).  0 = default for each (both modes: 64, 1, 2048 draws, sc1; K2
  * launches of >= 8 rounds of resident waves: 4096 draws; DG1 with a zero
- * prefix: 512 draws).
+ * prefix: 4 waves, 512 draws).
  * A tuning knob; results are identical. */
 int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int wgs_per_cu,
                              uint64_t min_lane_draws, int store_policy);
+/* Keystream launches (mode 0 / 1): workgroups are remapped so each XCD
+ * writes runs of `waves` adjacent waves' lane regions (power of two; at or
+ * below the waves per workgroup = the dispatcher's round-robin order; 0 =
+ * default: 16, DG1 with a zero prefix 32).  A tuning knob; results are
+ * identical. */
+int s3dg_set_keystream_xcd_group(s3dg_ctx *ctx, int mode, uint32_t waves);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
 /* Resident workgroups per CU the current settings give (HIP occupancy API). */
 int s3dg_query_occupancy(s3dg_ctx *ctx, int batch, int *wgs_per_cu);

@@ -61,7 +61,19 @@ constexpr uint64_t kDgenPrefixMinDraws = 512;
 // 5187 / 5409 for the round-1 DG1 shape of 128-B pieces and 2 waves).  With
 // 1024 draws per lane a 1 MiB DG1 block is 128 lanes, so whole waves fall
 // inside a zero prefix and skip the PRNG.
-constexpr KsShape kDefaultKsShape[2] = {{64, 4, 0, kStoreSC1}, {64, 4, 0, kStoreSC1}};
+// XCD groups (k_keystream remaps workgroups so each XCD writes runs of
+// adjacent waves' lane regions instead of every 8th workgroup) and 1-wave
+// workgroups (a finished wave frees its slot without waiting for three
+// others).  One process, interleaved (profiles/r02/diag/ks/ks_xcd_sweep.log):
+//   K2 80 GiB, 4096 draws:   4 waves, dealing order 6475 -> 1 wave, groups of 16: 6737 GB/s
+//   K2 8 GiB, 2048 draws:    6551 -> 7007
+//   DG1 c1 80 GiB / 8 GiB:   6409 / 6561 -> 6646 / 6774
+//   DG1 c2 (zero prefix, 512 draws): 6061 -> 6682 with 4 waves, groups of 32
+//                            (1 wave, groups of 16: 6251)
+constexpr int kDefaultKsXcdWaves = 16;
+constexpr KsShape kDefaultKsShape[2] = {{64, 1, 0, kStoreSC1, kDefaultKsXcdWaves},
+                                        {64, 1, 0, kStoreSC1, kDefaultKsXcdWaves}};
+constexpr int kDgenPrefixWaves = 4, kDgenPrefixXcdWaves = 32;
 
 // Launch state private to one stream: the tile-record map of tiled launches
 // and the batch-descriptor staging.  Launches on one stream are ordered by
@@ -109,6 +121,7 @@ struct s3dg_ctx {
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
     uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
+    bool ks_auto_waves[2] = {true, true}, ks_auto_xcd[2] = {true, true};          // not set by the caller
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // tile maps and batch staging, one set per stream (s3dg::StreamState)
@@ -409,9 +422,20 @@ int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wg
     const KsShape &def = kDefaultKsShape[mode];
     c->ks[mode].draws = draws ? draws : def.draws;
     c->ks[mode].waves = waves ? waves : def.waves;
+    c->ks_auto_waves[mode] = waves == 0;
     c->ks[mode].wgs_per_cu = wgs_per_cu;
     c->ks[mode].store = store_policy < 0 ? def.store : store_policy;
     c->ks_min_draws[mode] = min_lane_draws ? min_lane_draws : kDefaultKsMinDraws[mode];
+    return S3DG_OK;
+}
+
+int s3dg_set_keystream_xcd_group(s3dg_ctx *c, int mode, uint32_t waves) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (mode != 0 && mode != 1) return fail(S3DG_EINVAL, "mode must be 0 (keystream) or 1 (dgen)");
+    if (waves > 4096 || (waves & (waves - 1))) return fail(S3DG_EINVAL, "waves per XCD group must be 0 or a power of two <= 4096");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->ks[mode].xcd_waves = waves ? (int)waves : kDefaultKsXcdWaves;
+    c->ks_auto_xcd[mode] = waves == 0;
     return S3DG_OK;
 }
 
@@ -851,9 +875,9 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     if (mode == 1 && zero_prefix && min_draws == kDefaultKsMinDraws[1]) min_draws = kDgenPrefixMinDraws;
     if (mode == 0 && min_draws == kDefaultKsMinDraws[0] && nd >= 64 * kKsLongDraws) {
         // waves at 4096 draws per lane vs the chip's resident keystream waves
-        // (one 4-wave workgroup per CU at the default shape)
+        // (4 per CU: 64-draw stages take 33 KiB of LDS per wave)
         const uint64_t waves = nchunks * (nd / kKsLongDraws) / 64;
-        if (waves >= kKsLongRounds * (uint64_t)c->cus * (uint64_t)c->ks[0].waves) min_draws = kKsLongDraws;
+        if (waves >= kKsLongRounds * (uint64_t)c->cus * 4) min_draws = kKsLongDraws;
     }
     uint32_t lpc = 1;
     while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
@@ -959,7 +983,12 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     A.m_unique = fastmod_magic(U == nb ? 1u : (uint32_t)U);
     A.zf_num = f_num;
     A.zf_den = f_den;
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, c->ks[1], (hipStream_t)stream), "launch k_keystream(dgen)");
+    KsShape sh = c->ks[1];
+    if (f_num > 0) {   // zero-prefix launches (512-draw lanes): 4-wave workgroups, groups of 32 waves
+        if (c->ks_auto_waves[1]) sh.waves = kDgenPrefixWaves;
+        if (c->ks_auto_xcd[1]) sh.xcd_waves = kDgenPrefixXcdWaves;
+    }
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, (hipStream_t)stream), "launch k_keystream(dgen)");
     return S3DG_OK;
 }
 

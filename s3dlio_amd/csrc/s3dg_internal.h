@@ -129,6 +129,10 @@ struct KeystreamArgs {
     // its chunk chunk0 + c % cpo, written at dst + object*obj_stride, seeded
     // seed_base + object*seed_step
     uint64_t cpo, obj_stride, seed_step;
+    // workgroups per XCD group (power of two; 1 = the dispatcher's round-robin
+    // dealing): each full group of 8*xg workgroups is remapped so the xg
+    // workgroups one XCD receives take xg adjacent work units
+    uint32_t xg;
 };
 
 // k_keystream launch shape: draws staged per lane per iteration (16, 32, 64),
@@ -137,6 +141,7 @@ struct KeystreamArgs {
 struct KsShape {
     int draws, waves, wgs_per_cu;
     int store;             // kStorePlain / kStoreNT / kStoreSC1 / kStoreNTSC1
+    int xcd_waves;         // adjacent waves per XCD group (power of two; <= waves: dealing order)
 };
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
                            const KsShape &sh, hipStream_t s);

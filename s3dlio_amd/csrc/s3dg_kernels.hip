@@ -551,7 +551,20 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     // global lane gl -> chunk gl / lpc, lane-in-chunk gl % lpc (lpc: power of two;
     // lpc > 64 spreads one chunk over lpc/64 waves)
     const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
-    const uint64_t gl = ((uint64_t)blockIdx.x * W + w) * 64 + l;
+    // Workgroups are dealt round-robin to the 8 XCDs, so consecutive ones
+    // write through different L2s.  Each full group of 8*xg workgroups is
+    // remapped so the xg workgroups one XCD receives take xg adjacent work
+    // units: every XCD writes runs of xg*W*64 adjacent lane regions
+    // (the last, partial group keeps the dealing order).
+    uint64_t bid = blockIdx.x;
+    if (A.xg > 1) {
+        const uint32_t gs = (uint32_t)__builtin_ctz(A.xg);
+        if (((bid >> (gs + 3)) + 1) << (gs + 3) <= gridDim.x) {
+            const uint64_t x = bid & 7, k = bid >> 3;
+            bid = ((k >> gs) << (gs + 3)) + (x << gs) + (k & (A.xg - 1));
+        }
+    }
+    const uint64_t gl = (bid * W + w) * 64 + l;
     const uint64_t c = gl >> lsh;                                    // local chunk index
     const uint64_t cpo = A.cpo ? A.cpo : A.nchunks;
     const uint64_t ko = c / cpo;                                     // object within the launch
@@ -753,7 +766,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     }
 #if S3DG_KS_TRACE
     if (l == 0 && g_ks_trace) {
-        const uint64_t wi = (uint64_t)blockIdx.x * W + w;
+        const uint64_t wi = bid * W + w;
         g_ks_trace[2 * wi] = t_start;
         g_ks_trace[2 * wi + 1] = wall_clock64();
     }
@@ -959,10 +972,12 @@ hipError_t launch_fill_uniform_tiles_ablated(const LaunchCfg &lc, uint8_t *dst, 
     return batch_tiles(lc, dst, total_tiles, tshift, tiles, base_dev, s, true);
 }
 
-hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
+hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A0, const uint64_t *jtab,
                            const KsShape &sh, hipStream_t s) {
     (void)hipGetLastError();
     const uint32_t lds = occupancy_lds(sh.wgs_per_cu, ks_static_lds(sh.draws, sh.waves));
+    KeystreamArgs A = A0;
+    A.xg = sh.xcd_waves > sh.waves ? (uint32_t)(sh.xcd_waves / sh.waves) : 1u;
     hipError_t e;
     S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s);
     return e;

@@ -186,6 +186,11 @@ class Context:
         call("s3dg_set_keystream_shape", self._h, int(mode), int(draws), int(waves), int(wgs_per_cu),
              int(min_lane_draws), int(store_policy))
 
+    def set_keystream_xcd_group(self, mode: int, waves: int = 0) -> None:
+        """Keystream launches: each XCD writes runs of `waves` adjacent waves'
+        lane regions (power of two; 0 = default 16); results are identical."""
+        call("s3dg_set_keystream_xcd_group", self._h, int(mode), int(waves))
+
     def query_keystream_occupancy(self, mode: int = 0) -> int:
         out = ctypes.c_int()
         call("s3dg_query_keystream_occupancy", self._h, int(mode), ctypes.byref(out))

@@ -58,6 +58,8 @@ def _reset(ctx):
     ctx.set_stream_tiles(-1)
     ctx.set_keystream_shape(0)
     ctx.set_keystream_shape(1)
+    ctx.set_keystream_xcd_group(0, 0)
+    ctx.set_keystream_xcd_group(1, 0)
 
 
 @pytest.mark.parametrize("seed", range(12 * SOAK))
@@ -161,6 +163,7 @@ def test_fuzz_random_layout_keystream_dgen(gpu_ctx, torch, oracle, seed):
                 gpu_ctx.set_keystream_shape(mode, rnd.choice([0, 16, 32, 64]), rnd.choice([0, 1, 2, 4]),
                                             rnd.choice([0, 0, 1, 3]), rnd.choice([0, 64, 512, 4096]),
                                             rnd.choice([-1, 0, 1, 2, 3]))
+                gpu_ctx.set_keystream_xcd_group(mode, rnd.choice([0, 1, 2, 8, 16, 64, 256]))
             L = _size(rnd)
             chunk = rnd.choice([128, 1152, 65536, 2 << 20, (rnd.randint(1, 4096)) * 128])
             sb = rnd.getrandbits(64)

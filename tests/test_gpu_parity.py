@@ -442,6 +442,34 @@ def test_keystream_shapes_vs_oracle(gpu_ctx, torch, oracle, shape):
         gpu_ctx.set_keystream_shape(1)
 
 
+@pytest.mark.parametrize("waves,xcd", [(4, 1), (4, 16), (4, 64), (1, 16), (1, 256), (2, 8)])
+def test_keystream_xcd_groups_vs_oracle(gpu_ctx, torch, oracle, waves, xcd):
+    """XCD-grouped workgroup remap (s3dg_set_keystream_xcd_group): full groups
+    plus a ragged last group write the same bytes as the dealing order, K2 and
+    DG1, every byte against the oracle."""
+    try:
+        for mode in (0, 1):
+            gpu_ctx.set_keystream_shape(mode, 64, waves)
+            gpu_ctx.set_keystream_xcd_group(mode, xcd)
+        length, chunk, sb = 300 * 2**20 + 5, 2 * 2**20, 31
+        t = torch.full((length + 64,), GUARD, dtype=torch.uint8, device="cuda")
+        gpu_ctx.xoshiro_fill(t, length, chunk_bytes=chunk, seed_base=sb)
+        h = t.cpu().numpy()
+        assert np.array_equal(h[:length], oracle.xoshiro_chunks(length, chunk, sb))
+        assert (h[length:] == GUARD).all()
+        size, d, c, seed = 200 * 2**20 + 3, 2, 1, 77
+        t = torch.full((size + 64,), GUARD, dtype=torch.uint8, device="cuda")
+        gpu_ctx.dgen_fill(t, size, dedup=d, compress=c, seed=seed)
+        h = t.cpu().numpy()
+        fn, fd = P.compress_ratio(c)
+        assert np.array_equal(h[:size], oracle.dgen_fill(size, d, fn, fd, seed))
+        assert (h[size:] == GUARD).all()
+    finally:
+        for mode in (0, 1):
+            gpu_ctx.set_keystream_shape(mode)
+            gpu_ctx.set_keystream_xcd_group(mode, 0)
+
+
 def test_keystream_full_size_properties(gpu_ctx, torch, oracle):
     """8 GiB of 2 MiB chunks: sampled chunks bit-exact, bytes ~uniform."""
     n = 8 * 2**30

@@ -6,7 +6,7 @@ tools/batch_lab.py: "kind:waves:occ:pf:store[:tile];..." with kind in
 stream2 (cfg2 stream), stream3 (cfg3 stream), cfg4 (log-uniform batch),
 cfg7 (uniform 8 MiB batch), small (log-uniform 4 KiB-1 MiB batch), mid
 (uniform 1 MiB + 123 B batch), ceiling (store-only kernel), crc (s3dg_crc32),
-k2 (2 MiB keystream chunks; fields waves:wgs_per_cu:min_lane_draws:store).
+k2 (2 MiB keystream chunks; fields waves:wgs_per_cu:min_lane_draws:store[:xcd_waves]).
 
     LAB_VARIANTS=... python tools/variant_lab.py --build-only   # here
     LAB_VARIANTS=... LAB_POINTS=... python tools/variant_lab.py # GPU box
@@ -122,11 +122,15 @@ def main():
                 assert L.s3dg_set_occupancy(h, o, o) == 0
                 assert L.s3dg_set_batch_prefetch(h, u32(f)) == 0
                 assert L.s3dg_set_store_policy(h, sp, sp) == 0
-                assert L.s3dg_set_batch_tile(h, u32(tb)) == 0
+                if not (k.startswith("k2") or k.startswith("dg1")):
+                    assert L.s3dg_set_batch_tile(h, u32(tb)) == 0
                 if k.startswith("k2"):         # k2 / dg1: waves, wgs/CU, min lane draws, store
                     assert L.s3dg_set_keystream_shape(h, 0, 64, w, o, u64(f), sp) == 0
                 if k.startswith("dg1"):
                     assert L.s3dg_set_keystream_shape(h, 1, 64, w, o, u64(f), sp) == 0
+                if (k.startswith("k2") or k.startswith("dg1")) and hasattr(L, "s3dg_set_keystream_xcd_group"):
+                    for md in (0, 1):           # 6th field: waves per XCD group (0 = default)
+                        assert L.s3dg_set_keystream_xcd_group(h, md, u32(tb)) == 0
                 run(L, h, k)
                 torch.cuda.synchronize()
                 if k == "crc":
