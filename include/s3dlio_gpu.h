@@ -100,7 +100,7 @@ int s3dg_set_stream_tiles(s3dg_ctx *ctx, int on);
  * workgroups per CU cap (0 = none), draws per lane (>= 64; sets lanes per
  * chunk; launches too small to fill the GPU use shorter spans, down to 256), store cache policy (as s3dg_set_store_policy, negative =
  * default).  0 = default for each (both modes: 64, 1, 2048 draws, sc1; K2
- * launches of >= 8 rounds of resident waves: 4096 draws; DG1 with a zero
+ * launches of >= 4 rounds of resident waves: 4096 draws; DG1 with a zero
  * prefix: 4 waves, 512 draws).
  * A tuning knob; results are identical. */
 int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int wgs_per_cu,

@@ -45,11 +45,12 @@ constexpr int kDefaultStoreDense = kStoreNTSC1;
 // (K2 8 GiB launches 6096 -> 6621 GB/s, 80 GiB 6436 -> 6596; DG1 c1 6141 ->
 // 6604 / 6434 -> 6621; profiles/r02/diag/ks/ks_draws_sweep.log), and K2
 // launches of at least kKsLongRounds rounds of resident waves take 4096
-// (80 GiB: 6718; 8 GiB, 4 rounds: 6437, so not there).  DG1 stays at 2048:
+// (80 GiB: 6718; with 1-wave workgroups in XCD groups also 8 GiB launches,
+// profiles/r02/diag/ks/ks_draws_new_shape.log).  DG1 stays at 2048:
 // at 4096 a wave would span two 1 MiB blocks and lose the scalar jump.
 constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 2048};
 constexpr uint64_t kKsLongDraws = 4096;
-constexpr uint64_t kKsLongRounds = 8;
+constexpr uint64_t kKsLongRounds = 4;   // 1-wave workgroups: 8 GiB launches (4 rounds) 6755 -> 6986 GB/s at 4096
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
 // DG1 with a zero prefix (compress > 1): 512 draws per lane by default, so the
 // waves that skip the PRNG cover more of each block's prefix (d1 c2: 6413 ->
