@@ -80,6 +80,33 @@ def test_device_dgen_fill_stream_equals_per_object(S, oracle, gpu_ctx, size, str
     assert (got[(n - 1) * stride + size:] == 0xAB).all()
 
 
+def test_device_dgen_tail_part_vs_oracle(S, oracle, gpu_ctx):
+    """Launches of >= 1 GiB of DG1 blocks run their last round of chunks in
+    shorter lanes (the tail part).  One 1.5 GiB + 5 B object
+    every byte against the oracle, and three 600 MiB objects in one
+    s3dg_dgen_fill_stream launch (tail across objects) against three
+    s3dg_dgen_fill calls (different splits) and the oracle."""
+    import torch
+    size = 1536 * MiB + 5
+    t = torch.full((size + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    gpu_ctx.dgen_fill(t, size, dedup=1, compress=1, seed=123)
+    torch.cuda.synchronize()
+    h = t.cpu().numpy()
+    assert np.array_equal(h[:size], oracle.dgen_fill(size, 1, 0, 1, 123))
+    assert (h[size:] == 0xAB).all()
+    del t, h
+    size, n, sb = 600 * MiB, 3, 0x5EED000000000001
+    a = torch.full((n * size + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    gpu_ctx.dgen_fill_stream(a, size, n, dedup=3, compress=1, seed_base=sb)
+    b = torch.full_like(a, 0xAB)
+    for j in range(n):
+        gpu_ctx.dgen_fill(b[j * size:], size, dedup=3, compress=1, seed=S.object_entropy(sb, j))
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    got = a[(n - 1) * size:n * size].cpu().numpy()
+    assert np.array_equal(got, oracle.dgen_fill(size, 3, 0, 1, S.object_entropy(sb, n - 1)))
+
+
 def test_device_dgen_fill_stream_rejects_overlap(S, gpu_ctx):
     import torch
     buf = torch.empty(8 * MiB, dtype=torch.uint8, device="cuda")
