@@ -52,10 +52,6 @@ constexpr uint64_t kDefaultKsMinDraws[2] = {2048, 2048};
 constexpr uint64_t kKsLongDraws = 4096;
 constexpr uint64_t kKsLongRounds = 4;   // 1-wave workgroups: 8 GiB launches (4 rounds) 6755 -> 6986 GB/s at 4096
 constexpr uint64_t kKsMinSpan = 256;          // fewest draws per lane for small launches
-constexpr uint32_t kKsTailDiv = 4;            // tail part: lanes a quarter as long
-#ifndef S3DG_KS_NOTAIL
-#define S3DG_KS_NOTAIL 0                      // diagnostic builds: no tail part (A/B)
-#endif
 // DG1 with a zero prefix (compress > 1): 512 draws per lane by default, so the
 // waves that skip the PRNG cover more of each block's prefix (d1 c2: 6413 ->
 // 6694 GB/s; at c1 the extra jumps cost: 5896 -> 5347, profiles/r02/diag/k2_xcd.log)
@@ -898,45 +894,19 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     A.lpc = lpc;
     A.span = (uint32_t)span;
     std::lock_guard<std::mutex> g(c->mu);
-    auto table = [&](uint32_t lp, uint64_t sp, const uint64_t **out) -> int {
-        const uint64_t key = ((uint64_t)lp << 32) | sp;
-        auto it = c->jtabs.find(key);
-        if (it == c->jtabs.end()) {
-            std::vector<uint64_t> h(4 * (size_t)lp, 0);
-            for (uint32_t k = 0; k < lp; ++k)
-                if (!jump_poly((uint64_t)k * sp, &h[4 * k]))
-                    return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
-            uint64_t *d = nullptr;
-            HIP_TRY(hipMalloc(&d, h.size() * 8), "hipMalloc(jump table)");
-            HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(jump table)");
-            it = c->jtabs.emplace(key, d).first;
-        }
-        *out = it->second;
-        return S3DG_OK;
-    };
-    if (int r = table(lpc, span, jtab)) return r;
-    // Tail part: the chunks of the launch's last round of resident waves run
-    // in lanes a quarter as long, so the round drains in a quarter of the time
-    // (DESIGN.md §5.2).  Needs whole waves per chunk in both parts.
-    A.lpc2 = 0;
-    A.tsplit = nchunks;
-    A.span2 = 0;
-    A.jtab2 = nullptr;
-#if !S3DG_KS_NOTAIL
-    const uint64_t span2 = (span / kKsTailDiv + D - 1) / D * D;
-    if (lpc >= 64 && lpc * kKsTailDiv <= 1024 && span2 >= kKsMinSpan && nchunks >= 2 &&
-        (uint64_t)lpc * kKsTailDiv * span2 >= nd) {
-        const uint64_t resident_lanes = (uint64_t)c->cus * 4 * 64;
-        uint64_t k = resident_lanes / lpc;                    // chunks of one round
-        if (k > nchunks / 2) k = nchunks / 2;
-        if (k > 0) {
-            A.lpc2 = lpc * kKsTailDiv;
-            A.span2 = (uint32_t)span2;
-            A.tsplit = nchunks - k;
-            if (int r = table(A.lpc2, span2, &A.jtab2)) return r;
-        }
+    const uint64_t key = ((uint64_t)lpc << 32) | span;
+    auto it = c->jtabs.find(key);
+    if (it == c->jtabs.end()) {
+        std::vector<uint64_t> h(4 * (size_t)lpc, 0);
+        for (uint32_t k = 0; k < lpc; ++k)
+            if (!jump_poly((uint64_t)k * span, &h[4 * k]))
+                return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
+        uint64_t *d = nullptr;
+        HIP_TRY(hipMalloc(&d, h.size() * 8), "hipMalloc(jump table)");
+        HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(jump table)");
+        it = c->jtabs.emplace(key, d).first;
     }
-#endif
+    *jtab = it->second;
     return S3DG_OK;
 }
 

@@ -133,12 +133,6 @@ struct KeystreamArgs {
     // dealing): each full group of 8*xg workgroups is remapped so the xg
     // workgroups one XCD receives take xg adjacent work units
     uint32_t xg;
-    // tail part (lpc2 != 0): chunks [tsplit, nchunks) run with lpc2 lanes of
-    // span2 draws (jump table jtab2), so the launch's last round drains
-    // faster; lanes [0, tsplit*lpc) are the main part
-    uint64_t tsplit;
-    uint32_t lpc2, span2;
-    const uint64_t *jtab2;
 };
 
 // k_keystream launch shape: draws staged per lane per iteration (16, 32, 64),

@@ -547,6 +547,10 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     const uint32_t t = threadIdx.x, l = t & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
     uint8_t *myrows = rows[w];
+    const uint32_t lpc = A.lpc, span = A.span;
+    // global lane gl -> chunk gl / lpc, lane-in-chunk gl % lpc (lpc: power of two;
+    // lpc > 64 spreads one chunk over lpc/64 waves)
+    const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
     // Workgroups are dealt round-robin to the 8 XCDs, so consecutive ones
     // write through different L2s.  Each full group of 8*xg workgroups is
     // remapped so the xg workgroups one XCD receives take xg adjacent work
@@ -560,21 +564,8 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
             bid = ((k >> gs) << (gs + 3)) + (x << gs) + (k & (A.xg - 1));
         }
     }
-    // global lane gl -> chunk gl / lpc, lane-in-chunk gl % lpc (lpc: power of two;
-    // lpc > 64 spreads one chunk over lpc/64 waves).  Waves past the main
-    // part's lanes take the tail part: its chunks in shorter lanes.
-    uint32_t lpc = A.lpc, span = A.span;
-    const uint64_t *jt = jtab;
-    uint64_t gl = (bid * W + w) * 64 + l, c0 = 0;
-    if (A.lpc2 && (bid * W + w) * 64 >= A.tsplit * A.lpc) {
-        gl -= A.tsplit * A.lpc;
-        c0 = A.tsplit;
-        lpc = A.lpc2;
-        span = A.span2;
-        jt = A.jtab2;
-    }
-    const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
-    const uint64_t c = c0 + (gl >> lsh);                             // local chunk index
+    const uint64_t gl = (bid * W + w) * 64 + l;
+    const uint64_t c = gl >> lsh;                                    // local chunk index
     const uint64_t cpo = A.cpo ? A.cpo : A.nchunks;
     const uint64_t ko = c / cpo;                                     // object within the launch
     const uint64_t cl = c - ko * cpo;
@@ -652,7 +643,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         uint64_t u2 = readlane64(s2, 0), u3 = readlane64(s3, 0);
         // the lane's 256-bit polynomial in two loads up front (one load and
         // wait per 32 steps before)
-        const uint4 *Jv = reinterpret_cast<const uint4 *>(jt + 4 * sub);
+        const uint4 *Jv = reinterpret_cast<const uint4 *>(jtab + 4 * sub);
         const uint4 j0 = Jv[0], j1 = Jv[1];
         const uint32_t J[8] = {j0.x, j0.y, j0.z, j0.w, j1.x, j1.y, j1.z, j1.w};
         uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -674,7 +665,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
         // state <- sum over set bits i of J of step^i(state): 256 steps, the
         // polynomial read as 8 32-bit halves so each step's mask is one
         // sign-extended bit field and each accumulate one v_bitop3
-        const uint32_t *J = reinterpret_cast<const uint32_t *>(jt + 4 * sub);
+        const uint32_t *J = reinterpret_cast<const uint32_t *>(jtab + 4 * sub);
         uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
         for (int h = 0; h < 8; ++h) {
             const uint32_t jw = J[h];
@@ -785,8 +776,7 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
 template <int D, int W>
 hipError_t launch_ks_one(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab, uint32_t lds,
                          int store, hipStream_t s) {
-    const uint64_t lanes = A.lpc2 ? A.tsplit * A.lpc + (A.nchunks - A.tsplit) * A.lpc2 : A.nchunks * A.lpc;
-    const uint64_t waves = (lanes + 63) / 64;
+    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
     const uint64_t wgs = (waves + W - 1) / W;
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (store == kStoreSC1)

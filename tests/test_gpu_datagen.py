@@ -80,12 +80,12 @@ def test_device_dgen_fill_stream_equals_per_object(S, oracle, gpu_ctx, size, str
     assert (got[(n - 1) * stride + size:] == 0xAB).all()
 
 
-def test_device_dgen_tail_part_vs_oracle(S, oracle, gpu_ctx):
-    """Launches of >= 1 GiB of DG1 blocks run their last round of chunks in
-    shorter lanes (the tail part).  One 1.5 GiB + 5 B object
-    every byte against the oracle, and three 600 MiB objects in one
-    s3dg_dgen_fill_stream launch (tail across objects) against three
-    s3dg_dgen_fill calls (different splits) and the oracle."""
+def test_device_dgen_large_launches_vs_oracle(S, oracle, gpu_ctx):
+    """Launches of >= 1 GiB of DG1 blocks (the default lane shape, several
+    rounds of resident waves, XCD groups).  One 1.5 GiB + 5 B object every
+    byte against the oracle, and three 600 MiB objects in one
+    s3dg_dgen_fill_stream launch against three s3dg_dgen_fill calls (other
+    lane splits) and the oracle."""
     import torch
     size = 1536 * MiB + 5
     t = torch.full((size + 64,), 0xAB, dtype=torch.uint8, device="cuda")
