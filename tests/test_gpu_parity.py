@@ -470,6 +470,31 @@ def test_keystream_xcd_groups_vs_oracle(gpu_ctx, torch, oracle, waves, xcd):
             gpu_ctx.set_keystream_xcd_group(mode, 0)
 
 
+def test_keystream_two_chunks_per_wave_vs_oracle(gpu_ctx, torch, oracle):
+    """32 lanes per chunk (4096-draw lanes over 1 MiB chunks): every wave holds
+    two chunks and runs two scalar jump sequences.  Large enough that the
+    launch keeps 32 lanes per chunk; K2 and DG1, every byte vs the oracle."""
+    try:
+        for mode in (0, 1):
+            gpu_ctx.set_keystream_shape(mode, 64, 1, 0, 4096)
+        length, chunk, sb = 2 * 2**30 + 5, 2**20, 5
+        t = torch.full((length + 64,), GUARD, dtype=torch.uint8, device="cuda")
+        gpu_ctx.xoshiro_fill(t, length, chunk_bytes=chunk, seed_base=sb)
+        h = t.cpu().numpy()
+        assert np.array_equal(h[:length], oracle.xoshiro_chunks(length, chunk, sb))
+        assert (h[length:] == GUARD).all()
+        del t, h
+        size = 2 * 2**30 + 3
+        t = torch.full((size + 64,), GUARD, dtype=torch.uint8, device="cuda")
+        gpu_ctx.dgen_fill(t, size, dedup=2, compress=1, seed=17)
+        h = t.cpu().numpy()
+        assert np.array_equal(h[:size], oracle.dgen_fill(size, 2, 0, 1, 17))
+        assert (h[size:] == GUARD).all()
+    finally:
+        for mode in (0, 1):
+            gpu_ctx.set_keystream_shape(mode)
+
+
 def test_keystream_full_size_properties(gpu_ctx, torch, oracle):
     """8 GiB of 2 MiB chunks: sampled chunks bit-exact, bytes ~uniform."""
     n = 8 * 2**30
