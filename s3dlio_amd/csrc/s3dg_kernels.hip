@@ -661,38 +661,6 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
             }
         }
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
-    } else if (lpc == 32 && !(S3DG_KS_JUMP & 1)) {
-        // Two chunks per wave (lanes 0-31 and 32-63): two scalar sequences,
-        // each lane accumulating only its own half's states (16 v_bitop3 per
-        // step: a lane's mask is zero for the other half).
-        uint64_t u0 = readlane64(s0, 0), u1 = readlane64(s1, 0);
-        uint64_t u2 = readlane64(s2, 0), u3 = readlane64(s3, 0);
-        uint64_t v0 = readlane64(s0, 32), v1 = readlane64(s1, 32);
-        uint64_t v2 = readlane64(s2, 32), v3 = readlane64(s3, 32);
-        const uint32_t lo_half = l < 32 ? ~0u : 0u;
-        const uint4 *Jv = reinterpret_cast<const uint4 *>(jtab + 4 * sub);
-        const uint4 j0 = Jv[0], j1 = Jv[1];
-        const uint32_t J[8] = {j0.x, j0.y, j0.z, j0.w, j1.x, j1.y, j1.z, j1.w};
-        uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            const uint32_t jw = J[h];
-#pragma unroll 4
-            for (int b = 0; b < 32; ++b) {
-                const uint32_t m = (uint32_t)((int32_t)(jw << (31 - b)) >> 31);
-                const uint32_t ma = m & lo_half, mb = m & ~lo_half;
-                a0 = and_xor_64(u0, a0, ma); a1 = and_xor_64(u1, a1, ma);
-                a2 = and_xor_64(u2, a2, ma); a3 = and_xor_64(u3, a3, ma);
-                a0 = and_xor_64(v0, a0, mb); a1 = and_xor_64(v1, a1, mb);
-                a2 = and_xor_64(v2, a2, mb); a3 = and_xor_64(v3, a3, mb);
-                const uint64_t t = u1 << 17, tv = v1 << 17;
-                u2 ^= u0; u3 ^= u1; u1 ^= u2; u0 ^= u3; u2 ^= t;
-                u3 = rotl64(u3, 45);
-                v2 ^= v0; v3 ^= v1; v1 ^= v2; v0 ^= v3; v2 ^= tv;
-                v3 = rotl64(v3, 45);
-            }
-        }
-        s0 = a0; s1 = a1; s2 = a2; s3 = a3;
     } else if (lpc > 1 && sub > 0) {             // jump to draw sub*span
         // state <- sum over set bits i of J of step^i(state): 256 steps, the
         // polynomial read as 8 32-bit halves so each step's mask is one

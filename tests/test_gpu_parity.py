@@ -472,8 +472,10 @@ def test_keystream_xcd_groups_vs_oracle(gpu_ctx, torch, oracle, waves, xcd):
 
 def test_keystream_two_chunks_per_wave_vs_oracle(gpu_ctx, torch, oracle):
     """32 lanes per chunk (4096-draw lanes over 1 MiB chunks): every wave holds
-    two chunks and runs two scalar jump sequences.  Large enough that the
-    launch keeps 32 lanes per chunk; K2 and DG1, every byte vs the oracle."""
+    two chunks, so the lanes take the per-lane vector jump.  Large enough that
+    the launch keeps 32 lanes per chunk; K2 and DG1, every byte vs the oracle.
+    (Two scalar sequences per wave were tried: DG1 at 4096 draws ran no faster
+    than at 2048, profiles/r02/diag/ks/dg1_two_chunk_waves_ab.log.)"""
     try:
         for mode in (0, 1):
             gpu_ctx.set_keystream_shape(mode, 64, 1, 0, 4096)
