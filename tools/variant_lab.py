@@ -124,23 +124,24 @@ def main():
                 assert L.s3dg_set_store_policy(h, sp, sp) == 0
                 if not (k.startswith("k2") or k.startswith("dg1")):
                     assert L.s3dg_set_batch_tile(h, u32(tb)) == 0
+                ksd = int(k.split("@")[1]) if "@" in k else 64   # "k2@32": 32 draws per stage
                 if k.startswith("k2"):         # k2 / dg1: waves, wgs/CU, min lane draws, store
-                    assert L.s3dg_set_keystream_shape(h, 0, 64, w, o, u64(f), sp) == 0
+                    assert L.s3dg_set_keystream_shape(h, 0, ksd, w, o, u64(f), sp) == 0
                 if k.startswith("dg1"):
-                    assert L.s3dg_set_keystream_shape(h, 1, 64, w, o, u64(f), sp) == 0
+                    assert L.s3dg_set_keystream_shape(h, 1, ksd, w, o, u64(f), sp) == 0
                 if (k.startswith("k2") or k.startswith("dg1")) and hasattr(L, "s3dg_set_keystream_xcd_group"):
                     for md in (0, 1):           # 6th field: waves per XCD group (0 = default)
                         assert L.s3dg_set_keystream_xcd_group(h, md, u32(tb)) == 0
-                run(L, h, k)
+                run(L, h, k.split("@")[0])
                 torch.cuda.synchronize()
                 if k == "crc":
                     import time
                     t0 = time.perf_counter(); run(L, h, k); dt = time.perf_counter() - t0
                 else:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(st); run(L, h, k); e1.record(st); torch.cuda.synchronize()
+                    e0.record(st); run(L, h, k.split("@")[0]); e1.record(st); torch.cuda.synchronize()
                     dt = e0.elapsed_time(e1) * 1e-3
-                res.setdefault((name, pt), []).append(work[k] / dt / 1e9)
+                res.setdefault((name, pt), []).append(work[k.split("@")[0]] / dt / 1e9)
         print(f"rep {rep} done", flush=True)
     if crcs:
         print(json.dumps({"crc_values_per_variant": {n: sorted(crcs.get(libs[n][0], [])) for n in libs}}))
