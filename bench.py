@@ -81,7 +81,19 @@ CONFIGS = {
              kind="dgen_stream", n=10, size=8 * GiB, dedup=1, compress=1, scaling="weak"),
     17: dict(name="dg1 stream: 10 x 8 GiB DG1 objects in one s3dg_dgen_fill_stream launch, dedup=2 compress=2",
              kind="dgen_stream", n=10, size=8 * GiB, dedup=2, compress=2, scaling="weak"),
+    # the host-buffer drop-ins (the reference's own API: host memory in, host memory out)
+    18: dict(name="host: 1000 x s3dlio_fill_controlled_data on one 1 MiB host buffer, d1 c1 (criterion shape)",
+             kind="host", n=1000, size=1 * MiB, dedup=1, compress=1, scaling="weak"),
+    19: dict(name="host: 500 x s3dlio_fill_controlled_data on one 4 MiB host buffer, d1 c1 (criterion shape)",
+             kind="host", n=500, size=4 * MiB, dedup=1, compress=1, scaling="weak"),
+    20: dict(name="host: 200 x s3dlio_fill_controlled_data on one 16 MiB host buffer, d1 c1 (criterion shape)",
+             kind="host", n=200, size=16 * MiB, dedup=1, compress=1, scaling="weak"),
+    21: dict(name="host: 8 x s3dlio_fill_controlled_data on one 1 GiB host buffer, d1 c1 (split over host slots)",
+             kind="host", n=8, size=1 * GiB, dedup=1, compress=1, scaling="weak"),
+    22: dict(name="host: generate_into_buffer (s3dg_generate_data) from 8 threads, 8 MiB each, 100 calls per thread",
+             kind="host", n=100, size=8 * MiB, threads=8, dedup=1, compress=1, scaling="weak"),
 }
+PCIE_PEAK_GBS = 63.0    # PCIe Gen5 x16, one direction, before protocol overhead
 
 
 def log_uniform_sizes(n: int, seed: int = 4, lo: int = 4096, hi: int = 64 * MiB) -> list[int]:
@@ -124,6 +136,8 @@ def parse():
     p.add_argument("--d2h-reps", type=int, default=1, help="D2H-inclusive samples (diagnosis of run-to-run spread)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-ceiling", action="store_true")
+    p.add_argument("--host-mem", choices=["pageable", "pinned"], default="pageable",
+                   help="host configs (18-22): the caller's buffer is pageable (a reused Vec / bytearray) or pinned")
     p.add_argument("--device-override", type=int, default=None,
                    help="rehearsal only: put every rank on this device (e.g. 8 ranks on a 1-GPU box)")
     return p.parse_args()
@@ -302,6 +316,34 @@ def main() -> int:
         launches.append((single_step, calls * size))
         samples = [(0, ("single", size))]
         step_bytes = calls * size
+    elif kind == "host":
+        # synchronous host-buffer calls from a native loop; the work runs on
+        # the library's host slots (S3DLIO_GPU_DEVICE(S)), timed by wall clock
+        size, calls, nthr = cfg["size"], args.objects or cfg["n"], cfg.get("threads", 1)
+        nl = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libnative_loop.so"))
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        nl.nl_host_fill_loop.argtypes = [vp, vp, u64, u64, u64, u64]
+        nl.nl_threads_gen_loop.argtypes = [vp, ctypes.POINTER(vp), u64, ctypes.c_int, u64, u64, u64]
+        hbufs = [host_buffer(size, args.host_mem, call) for _ in range(nthr)]
+        ring = None
+        if nthr == 1:
+            fptr = ctypes.cast(lib.s3dlio_fill_controlled_data, vp)
+
+            def host_step(b=hbufs[0][0]):
+                r = nl.nl_host_fill_loop(fptr, b, size, calls, d, cfg["compress"])
+                if r:
+                    raise RuntimeError(f"s3dlio_fill_controlled_data failed ({r}): {lib.s3dg_last_error().decode()}")
+        else:
+            gptr = ctypes.cast(lib.s3dg_generate_data, vp)
+            arr = (vp * nthr)(*[b for b, _ in hbufs])
+
+            def host_step():
+                r = nl.nl_threads_gen_loop(gptr, arr, size, nthr, calls, d, cfg["compress"])
+                if r:
+                    raise RuntimeError(f"s3dg_generate_data failed ({r}): {lib.s3dg_last_error().decode()}")
+        launches.append((host_step, calls * nthr * size))
+        samples = [(0, ("host", size, nthr))]
+        step_bytes = calls * nthr * size
     elif kind == "dgen_stream":   # DG1 objects, one launch per ring pass
         size = cfg["size"]
         ring_objs = max(1, min(n_rank, ring_cap // size))
@@ -330,7 +372,14 @@ def main() -> int:
     tiled = (kind == "stream" and args.stream_tiles != 0
              and all(b // cfg["size"] * ((cfg["size"] + 4095) // 4096) >= 16384 for _, b in launches)
              and cfg["size"] % (32 * KiB) == 0)
-    if kind == "keystream":
+    if kind == "host":
+        kernel, launch_shape = ("k_fill_stream + hipMemcpyAsync D2H on the host slots' staging streams"
+                                if cfg.get("threads", 1) == 1 else
+                                "k_keystream (DG1) + hipMemcpyAsync D2H on the host slots' staging streams"), (
+            f"{cfg.get('threads', 1)} caller thread(s), {args.host_mem} host buffer, slots "
+            f"{os.environ.get('S3DLIO_GPU_DEVICES') or os.environ.get('S3DLIO_GPU_DEVICE') or 'every visible GPU'}, "
+            f"D2H mode {os.environ.get('S3DLIO_HOST_D2H', 'direct')}")
+    elif kind == "keystream":
         kernel, launch_shape = "k_keystream", ("k_keystream<64,1>: 64 lanes x 4096 draws per 2 MiB chunk "
                                                "(jump-ahead, state sequence on the scalar unit), 64-draw LDS stage "
                                                "per lane, 512-B row pieces per store, 1-wave workgroups in XCD "
@@ -374,13 +423,15 @@ def main() -> int:
     t1 = time.perf_counter()
     elapsed = cp.max(t1 - t0)
     kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(0, len(evs), 2)]
+    if kind == "host":     # synchronous calls on the library's own streams: wall clock
+        kern_ms = [(t1 - t0) * 1e3 / args.steps] * args.steps
     launch_bytes = [b for _, b in launches] * args.steps
     avg_ms = sum(kern_ms) / len(kern_ms)
     achieved_gbs = sum(launch_bytes) / (sum(kern_ms) * 1e-3) / 1e9
-    if kind == "single":                       # one "launch" = one call
+    if kind in ("single", "host"):             # one "launch" = one call
         avg_ms /= launches[0][1] // cfg["size"]
     algo_per_launch = int(sum(launch_bytes) / len(launch_bytes))
-    if kind == "single":
+    if kind in ("single", "host"):
         algo_per_launch = cfg["size"]
 
     total_bytes = cp.sum(step_bytes) * args.steps
@@ -401,7 +452,8 @@ def main() -> int:
     # ---- verification: sampled objects of the last writes vs the C oracle ---------------
     verified = None
     if not args.no_verify:
-        verified = verify(torch, ring, samples, cfg, fn, fd, rank, cp)
+        verified = (verify_host(hbufs, cfg, fn, fd, call, cp) if kind == "host"
+                    else verify(torch, ring, samples, cfg, fn, fd, rank, cp))
 
     # ---- write ceilings on the same buffer ----------------------------------------------
     ceil = None
@@ -427,7 +479,14 @@ def main() -> int:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes)
 
-    if rank == 0:
+    if rank == 0 and kind == "host":
+        # the host-buffer path is bound by the PCIe link, not HBM
+        roof = {"bound": "pcie", "achieved": round(achieved_gbs, 1), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved_gbs / PCIE_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
+                "launch_shape": launch_shape, "avg_call_ms": round(avg_ms, 4),
+                "algorithmic_bytes_per_call": algo_per_launch, "host_mem": args.host_mem,
+                "source_digest": source_digest()}
+    elif rank == 0:
         roof = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic_from_profiles(args.config, algo_per_launch),
@@ -470,6 +529,41 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     cp.close()
     return 0
+
+
+def host_buffer(n: int, kind: str, call):
+    """(address, keepalive) of an n-byte host buffer, touched once (a reused
+    Vec / bytearray: pageable; or pinned by the library)."""
+    import numpy as np
+    if kind == "pinned":
+        p = ctypes.c_void_p()
+        call("s3dg_host_alloc_pinned", n, ctypes.byref(p))
+        ctypes.memset(p.value, 1, n)
+        return p.value, p
+    a = np.ones(n, np.uint8)
+    return int(a.ctypes.data), a
+
+
+def verify_host(hbufs, cfg, fn, fd, call, cp) -> bool:
+    """The host path's seeded forms into the same buffer, byte for byte against
+    the C oracle: fill_controlled_data_seeded (entropy 7, the slot context's
+    default base block) or generate_data (DG1, seed 7)."""
+    import numpy as np
+    from oracle import oracle_c as OC
+    size = cfg["size"]
+    b = hbufs[0][0]
+    got = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(b))
+    if cfg.get("threads", 1) == 1:
+        call("s3dlio_fill_controlled_data_seeded", b, size, cfg["dedup"], cfg["compress"], 7, None)
+        exp = OC.fill_controlled(size, cfg["dedup"], fn, fd, 7, OC.base_block(BASE_SEED))
+    else:
+        call("s3dg_generate_data", b, size, cfg["dedup"], cfg["compress"], 1, 7)
+        exp = OC.dgen_fill(size, cfg["dedup"], fn, fd, 7)
+    ok = sha(got) == sha(exp)
+    verified = bool(cp.max(0.0 if ok else 1.0) == 0.0)
+    if not verified:
+        print("bench: VERIFICATION FAILED: host-buffer output differs from the oracle", file=sys.stderr)
+    return verified
 
 
 def verify(torch, ring, samples, cfg, fn, fd, rank, cp) -> bool:
@@ -688,6 +782,23 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes):
     kind = cfg["kind"]
     meta = {"cores": threads, "kind": "port", "affinity_cpus": share["affinity_cpus"],
             "cgroup_quota_cpus": share["cgroup_quota_cpus"]}
+    if kind == "host" and cfg.get("threads", 1) == 1:
+        # the criterion loop: one reused buffer, one call at a time, over a
+        # persistent pool (Rayon's global pool) of the host's share of CPUs
+        size = cfg["size"]
+        buf = np.ones(size, np.uint8)
+        OC.pool_fill_controlled(buf, cfg["dedup"], fn, fd, 0, base, threads)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            used = OC.pool_fill_controlled(buf, cfg["dedup"], fn, fd, done + 1, base, threads)
+            done += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds:
+                break
+        meta["cores"] = used
+        return dict(meta, value=round(done * size / dt / GiB, 2), unit="GiB/s",
+                    sample=f"{done} fill_controlled_data calls on one reused {size // MiB} MiB host buffer over "
+                           f"{dt:.1f} s, persistent pool of {used} threads over 4 KiB blocks; {cpu_model()}")
     if kind in ("stream", "single") or (kind == "batch" and cfg.get("uniform")):
         # fill_controlled_data's par_chunks_mut(4096) over a reused 1 GiB ring
         # (uniform batches: the same objects, laid out back to back)
@@ -725,6 +836,15 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes):
                                     base.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
             return pos + (sz + 4095) // 4096 * 4096, sz
         what = "objects of the config's sizes, one object per task"
+    elif kind == "host":     # generate_into_buffer from several threads: DG1 objects, one per call
+        ring, nthr = cfg["size"], cfg["threads"]
+        threads = nthr
+        meta["cores"] = nthr
+
+        def work(buf, pos, j):
+            OC.dgen_fill(ring, cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, j), out=buf)
+            return 0, ring
+        what = f"{ring // MiB} MiB DG1 objects, one generate_into_buffer-shaped call per task"
     elif kind == "keystream":
         ring = 256 * MiB
 

@@ -322,10 +322,17 @@ int s3dg_put_objects_multi(s3dg_ctx *const *ctxs, uint32_t nctx, const char *con
  * one range per slot generated in parallel.  Bytes never depend on the slot.
  * Slot devices: env S3DLIO_GPU_DEVICE=k pins every call to GPU k;
  * S3DLIO_GPU_DEVICES=a,b,... lists them (repeats: several slots on one GPU);
- * neither: every visible GPU. */
+ * neither: every visible GPU, or, in one rank of a multi-process job
+ * (WORLD_SIZE > 1 and LOCAL_RANK set), that rank's GPU (LOCAL_RANK mod the
+ * device count) only.  Env S3DLIO_HOST_D2H=staged copies through pinned
+ * bounce buffers instead of straight into the caller's memory. */
 /* The slot device list for the given env values and device count (pure
  * function; no GPU needed).  *n <= cap entries written to out. */
 int s3dg_host_parse_devices(const char *pin, const char *list, int ndev, int *out, int cap, int *n);
+/* The same with the multi-process job's LOCAL_RANK / WORLD_SIZE values (NULL:
+ * unset); the library's own slot list is this function of its environment. */
+int s3dg_host_parse_devices_env(const char *pin, const char *list, const char *local_rank,
+                                const char *world_size, int ndev, int *out, int cap, int *n);
 int s3dg_host_slot_count(int *out);
 int s3dg_host_slot_device(int slot, int *device);
 /* The slot's context (owned by the pool: never destroy it); slot < 0 takes

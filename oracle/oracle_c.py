@@ -54,6 +54,8 @@ def lib():
         L.s3dgo_fill_stream_mt.argtypes = [u8p, u64, u64, u64, u64, u64, u64, u64, u64,
                                            u8p, ctypes.c_int]
         L.s3dgo_fill_stream_mt.restype = ctypes.c_int
+        L.s3dgo_pool_fill_controlled.argtypes = [u8p, u64, u64, u64, u64, u64, u8p, ctypes.c_int]
+        L.s3dgo_pool_fill_controlled.restype = ctypes.c_int
         L.s3dgo_xoshiro_chunks.argtypes = [u8p, u64, u64, u64]
         L.s3dgo_dgen_fill.argtypes = [u8p, u64, u64, u64, u64, u64]
         L.s3dgo_random_data.argtypes = [u8p, u64, u64, u8p]
@@ -101,6 +103,15 @@ def fill_controlled(length: int, dedup: int, f_num: int, f_den: int, entropy: in
     base = np.ascontiguousarray(base, np.uint8)
     lib().s3dgo_fill_controlled(_ptr(out), length, dedup, f_num, f_den, entropy, _ptr(base))
     return out
+
+
+def pool_fill_controlled(out: np.ndarray, dedup: int, f_num: int, f_den: int, entropy: int,
+                         base: np.ndarray, threads: int) -> int:
+    """One fill_controlled_data call on `out` over a persistent thread pool
+    (the CPU baseline of the reference's criterion shape); returns threads used."""
+    base = np.ascontiguousarray(base, np.uint8)
+    return lib().s3dgo_pool_fill_controlled(_ptr(out), out.size, dedup, f_num, f_den,
+                                            entropy & (2**64 - 1), _ptr(base), threads)
 
 
 def fill_stream(obj_size: int, n: int, dedup: int, f_num: int, f_den: int,

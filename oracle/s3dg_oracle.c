@@ -182,17 +182,18 @@ void s3dgo_fill_stream(uint8_t *dst, uint64_t obj_size, uint64_t stride, uint64_
 typedef struct {
     uint8_t *dst; uint64_t obj_size, stride, n, nblocks, unique;
     const uint64_t *cl; uint64_t seed_base, first_obj; const uint8_t *base;
-    _Atomic uint64_t next; uint64_t total;
+    _Atomic uint64_t next; uint64_t total, grain;
 } mt_job;
 
 #define MT_GRAIN 64u
 
 static void *mt_worker(void *arg) {
     mt_job *J = (mt_job *)arg;
+    const uint64_t grain = J->grain ? J->grain : MT_GRAIN;
     for (;;) {
-        uint64_t g0 = atomic_fetch_add(&J->next, MT_GRAIN);
+        uint64_t g0 = atomic_fetch_add(&J->next, grain);
         if (g0 >= J->total) break;
-        uint64_t g1 = g0 + MT_GRAIN < J->total ? g0 + MT_GRAIN : J->total;
+        uint64_t g1 = g0 + grain < J->total ? g0 + grain : J->total;
         for (uint64_t g = g0; g < g1; ++g) {
             uint64_t j = g / J->nblocks, i = g % J->nblocks;
             uint64_t off = i * S3DGO_BLK;
@@ -218,6 +219,7 @@ int s3dgo_fill_stream_mt(uint8_t *dst, uint64_t obj_size, uint64_t stride, uint6
     J.cl = cl; J.seed_base = seed_base; J.first_obj = first_obj; J.base = base;
     atomic_init(&J.next, 0);
     J.total = J.nblocks * n;
+    J.grain = MT_GRAIN;
     pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
     int started = 0;
     for (int t = 1; t < threads; ++t)
@@ -227,6 +229,83 @@ int s3dgo_fill_stream_mt(uint8_t *dst, uint64_t obj_size, uint64_t stride, uint6
     free(tid);
     free(cl);
     return started + 1;
+}
+
+/* ---- persistent pool: the reference's criterion shape --------------------- */
+/* benches/performance_microbenchmarks.rs:43-64 calls fill_controlled_data on
+ * one reused 1/4/16 MiB Vec in a loop, on Rayon's global pool, which lives for
+ * the process.  Creating threads per call (s3dgo_fill_stream_mt) would charge
+ * each 1 MiB call tens of microseconds of pthread_create, so this form keeps
+ * `threads - 1` workers parked on a condition variable; the calling thread
+ * works too.  Blocks go out in grains of total / (8 * threads) (1..64), close
+ * to Rayon's adaptive splitting of par_chunks_mut. */
+static struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int workers;
+    int helpers;            /* workers 0 .. helpers-1 take part in the current job */
+    _Atomic uint64_t gen;
+    mt_job *job;
+    _Atomic int busy;
+} g_pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, 0, NULL, 0};
+
+static void *pool_worker(void *arg) {
+    const int id = (int)(intptr_t)arg;
+    uint64_t seen = 0;
+    for (;;) {
+        /* spin a while before parking, as Rayon's workers do, so back-to-back
+           calls do not pay a futex wake each */
+        for (int k = 0; k < 200000 && atomic_load_explicit(&g_pool.gen, memory_order_acquire) == seen; ++k)
+            __builtin_ia32_pause();
+        pthread_mutex_lock(&g_pool.mu);
+        while (atomic_load(&g_pool.gen) == seen) pthread_cond_wait(&g_pool.cv, &g_pool.mu);
+        seen = atomic_load(&g_pool.gen);
+        mt_job *J = g_pool.job;
+        const int part = id < g_pool.helpers;
+        pthread_mutex_unlock(&g_pool.mu);
+        if (part) mt_worker(J);
+        atomic_fetch_sub(&g_pool.busy, 1);
+    }
+    return NULL;
+}
+
+/* One fill_controlled_data call on `buf` (seeded by `entropy`) over the pool;
+ * not reentrant (one caller at a time).  Returns the threads used. */
+int s3dgo_pool_fill_controlled(uint8_t *buf, uint64_t len, uint64_t dedup, uint64_t f_num,
+                               uint64_t f_den, uint64_t entropy, const uint8_t *base, int threads) {
+    if (len == 0) return 0;
+    if (threads < 1) threads = 1;
+    pthread_mutex_lock(&g_pool.mu);
+    while (g_pool.workers < threads - 1) {
+        pthread_t t;
+        if (pthread_create(&t, NULL, pool_worker, (void *)(intptr_t)g_pool.workers) != 0) break;
+        pthread_detach(t);
+        ++g_pool.workers;
+    }
+    const int helpers = g_pool.workers < threads - 1 ? g_pool.workers : threads - 1;
+    pthread_mutex_unlock(&g_pool.mu);
+    mt_job J;
+    J.dst = buf; J.obj_size = len; J.stride = len; J.n = 1;
+    J.nblocks = (len + S3DGO_BLK - 1) / S3DGO_BLK;
+    J.unique = s3dgo_unique_blocks(J.nblocks, dedup);
+    uint64_t *cl = const_len_table(J.unique, f_num, f_den);
+    J.cl = cl; J.seed_base = entropy; J.first_obj = 0; J.base = base;
+    atomic_init(&J.next, 0);
+    J.total = J.nblocks;
+    uint64_t grain = J.total / (8u * (uint64_t)threads);
+    J.grain = grain < 1 ? 1 : (grain > MT_GRAIN ? MT_GRAIN : grain);
+    /* every parked worker wakes and checks in; only the first `helpers` work */
+    pthread_mutex_lock(&g_pool.mu);
+    g_pool.helpers = helpers;
+    atomic_store(&g_pool.busy, g_pool.workers);
+    g_pool.job = &J;
+    atomic_fetch_add_explicit(&g_pool.gen, 1, memory_order_release);
+    pthread_cond_broadcast(&g_pool.cv);
+    pthread_mutex_unlock(&g_pool.mu);
+    mt_worker(&J);
+    while (atomic_load(&g_pool.busy) > 0) { }
+    free(cl);
+    return helpers + 1;
 }
 
 /* ---- generate_npz_bytes_raw x-fill (src/data_formats/npz.rs:376-383) ----- */

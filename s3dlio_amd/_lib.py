@@ -95,6 +95,8 @@ SIGNATURES = {
     "s3dg_gen_slot": (c_int, [c_vp]),
     "s3dg_host_parse_devices": (c_int, [ctypes.c_char_p, ctypes.c_char_p, c_int, ctypes.POINTER(c_int), c_int,
                                         ctypes.POINTER(c_int)]),
+    "s3dg_host_parse_devices_env": (c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, c_int,
+                                            ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_int)]),
     "s3dg_host_slot_count": (c_int, [ctypes.POINTER(c_int)]),
     "s3dg_host_slot_device": (c_int, [c_int, ctypes.POINTER(c_int)]),
     "s3dg_host_slot_context": (c_int, [c_int, ctypes.POINTER(c_vp)]),

@@ -69,7 +69,7 @@ def build_native_loop(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(NL_LIB) and os.path.getmtime(NL_LIB) >= os.path.getmtime(NL_SRC):
         return NL_LIB
     os.makedirs(os.path.dirname(NL_LIB), exist_ok=True)
-    cmd = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Werror", "-o", NL_LIB, NL_SRC]
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Werror", "-o", NL_LIB, NL_SRC, "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

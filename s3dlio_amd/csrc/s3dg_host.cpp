@@ -18,7 +18,15 @@
 //     one per slot, generated in parallel (one host thread per extra slot).
 // Slot devices: S3DLIO_GPU_DEVICE=k pins every call to GPU k;
 // S3DLIO_GPU_DEVICES=a,b,... lists them (repeats give several slots on one
-// GPU); neither set: every visible GPU.  Bytes never depend on the slot.
+// GPU); neither set: every visible GPU, except in one rank of a multi-process
+// job (WORLD_SIZE > 1 and LOCAL_RANK set, as torch.distributed.run exports),
+// which keeps to its own GPU (LOCAL_RANK mod the visible count) so ranks do not
+// spread onto each other's devices.  Bytes never depend on the slot.
+// D2H mode (S3DLIO_HOST_D2H): "direct" (default) copies each device chunk
+// straight into the caller's buffer (hipMemcpyAsync; HIP stages pageable
+// memory itself); "staged" copies into a pinned bounce buffer of the staging
+// set and from there into the caller's buffer with host threads, overlapped
+// with the next chunk (DESIGN.md §5.8 has the A/B).
 #include "s3dg_internal.h"
 #include "s3dlio_gpu.h"
 
@@ -92,8 +100,8 @@ int pool_init(Pool &P) {
     H_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
     if (ndev <= 0) return s3dg_internal_fail(S3DG_EHIP, "no GPU visible");
     int devs[kMaxSlots], n = 0;
-    if (int r = s3dg_host_parse_devices(getenv("S3DLIO_GPU_DEVICE"), getenv("S3DLIO_GPU_DEVICES"), ndev, devs,
-                                        kMaxSlots, &n))
+    if (int r = s3dg_host_parse_devices_env(getenv("S3DLIO_GPU_DEVICE"), getenv("S3DLIO_GPU_DEVICES"),
+                                            getenv("LOCAL_RANK"), getenv("WORLD_SIZE"), ndev, devs, kMaxSlots, &n))
         return r;
     for (int k = 0; k < 2; ++k)
         if (int r = random_bytes(P.proc_base[k], kBlk)) return r;
@@ -146,9 +154,38 @@ void staging_free(HostStaging *sg) {
     for (int q = 0; q < 2; ++q) {
         if (sg->buf[q]) (void)hipFree(sg->buf[q]);
         if (sg->st[q]) (void)hipStreamDestroy(sg->st[q]);
+        if (sg->pin[q]) (void)hipHostFree(sg->pin[q]);
     }
     if (sg->base_user) (void)hipFree(sg->base_user);
     delete sg;
+}
+
+bool d2h_staged() {
+    static const bool staged = [] {
+        const char *v = getenv("S3DLIO_HOST_D2H");
+        return v && strcmp(v, "staged") == 0;
+    }();
+    return staged;
+}
+
+// memcpy of n bytes split over up to 8 threads (>= 8 MiB per part): one host
+// thread copies 10-20 GB/s, below one PCIe link.
+void par_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
+    constexpr uint64_t kPart = 8ull << 20;
+    uint64_t parts = n / kPart;
+    if (parts > 8) parts = 8;
+    if (parts < 2) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const uint64_t per = (n / parts + 4095) / 4096 * 4096;
+    std::thread th[8];
+    for (uint64_t p = 1; p < parts; ++p) {
+        const uint64_t lo = p * per, hi = p + 1 == parts ? n : (p + 1) * per;
+        th[p] = std::thread([=] { memcpy(dst + lo, src + lo, hi - lo); });
+    }
+    memcpy(dst, src, per);
+    for (uint64_t p = 1; p < parts; ++p) th[p].join();
 }
 
 const void *base_for(Slot *S, HostStaging *sg, const HostJob &J) {
@@ -220,18 +257,29 @@ void host_staging_release(HostStaging *sg) {
 // Bytes [pos, pos+n) of the job's object into host `buf` on the staging set's
 // slot: the covering generation blocks go through the two device chunks on
 // two streams (chunk k+1's kernel overlaps chunk k's D2H), then exactly the
-// requested bytes are copied out.
-int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
-    if (n == 0) return S3DG_OK;
-    Slot *S = pool().slots[sg->slot];
-    DeviceScope ds(S->device);
-    H_TRY(ds.err, "hipSetDevice");
+// requested bytes are copied out (directly, or through the pinned bounce
+// buffers in staged mode, where chunk k's host copy overlaps chunk k+1's
+// kernel and D2H).  On an error the streams are drained before returning, so
+// no copy is still landing in `buf` when the caller sees the failure.
+static int host_run_chunks(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
     if (J.base == HostJob::kBaseUser)
         H_TRY(hipMemcpy(sg->base_user, J.user_base, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
     const void *base = base_for(S, sg, J);
+    const bool staged = d2h_staged();
+    if (staged)
+        for (int q = 0; q < 2; ++q)
+            if (!sg->pin[q]) H_TRY(hipHostMalloc(&sg->pin[q], kChunk, hipHostMallocDefault), "hipHostMalloc(bounce)");
     const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
     const uint64_t per = kChunk / unit;
     const uint64_t b0 = pos / unit, b1 = (pos + n + unit - 1) / unit;
+    uint64_t pend_lo[2] = {0, 0}, pend_len[2] = {0, 0};   // staged: copied-out ranges per bounce buffer
+    auto drain = [&](int sl) -> int {                      // staged: bounce buffer sl -> buf
+        if (!pend_len[sl]) return S3DG_OK;
+        H_TRY(hipStreamSynchronize(sg->st[sl]), "hipStreamSynchronize");
+        par_copy(buf + (pend_lo[sl] - pos), (const uint8_t *)sg->pin[sl], pend_len[sl]);
+        pend_len[sl] = 0;
+        return S3DG_OK;
+    };
     int k = 0;
     for (uint64_t pb = b0; pb < b1; pb += per, ++k) {
         const uint64_t pe = pb + per < b1 ? pb + per : b1;
@@ -247,13 +295,35 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
         }
         const uint64_t lo = pb * unit > pos ? pb * unit : pos;
         const uint64_t hi = pe * unit < pos + n ? pe * unit : pos + n;
-        H_TRY(hipMemcpyAsync(buf + (lo - pos), (uint8_t *)sg->buf[sl] + (lo - pb * unit), hi - lo,
-                             hipMemcpyDeviceToHost, sg->st[sl]),
-              "hipMemcpyAsync(D2H)");
+        const uint8_t *src = (uint8_t *)sg->buf[sl] + (lo - pb * unit);
+        if (staged) {
+            H_TRY(hipMemcpyAsync(sg->pin[sl], src, hi - lo, hipMemcpyDeviceToHost, sg->st[sl]), "hipMemcpyAsync(D2H)");
+            pend_lo[sl] = lo;
+            pend_len[sl] = hi - lo;
+            if (int r = drain(sl ^ 1)) return r;          // chunk k-1, while chunk k runs
+        } else {
+            H_TRY(hipMemcpyAsync(buf + (lo - pos), src, hi - lo, hipMemcpyDeviceToHost, sg->st[sl]),
+                  "hipMemcpyAsync(D2H)");
+        }
+    }
+    if (staged) {
+        for (int q = 0; q < 2; ++q)
+            if (int r = drain((k + q) & 1)) return r;     // oldest first
     }
     H_TRY(hipStreamSynchronize(sg->st[0]), "hipStreamSynchronize");
     H_TRY(hipStreamSynchronize(sg->st[1]), "hipStreamSynchronize");
     return S3DG_OK;
+}
+
+int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
+    if (n == 0) return S3DG_OK;
+    Slot *S = pool().slots[sg->slot];
+    DeviceScope ds(S->device);
+    H_TRY(ds.err, "hipSetDevice");
+    const int r = host_run_chunks(sg, S, J, buf, pos, n);
+    if (r != S3DG_OK)
+        for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);   // nothing lands later
+    return r;
 }
 
 // The same, cut into one contiguous range per slot when the request is large
@@ -319,6 +389,11 @@ static int controlled_job(HostJob &J, uint64_t len, uint64_t dedup, uint64_t com
 extern "C" {
 
 int s3dg_host_parse_devices(const char *pin, const char *list, int ndev, int *out, int cap, int *n) {
+    return s3dg_host_parse_devices_env(pin, list, nullptr, nullptr, ndev, out, cap, n);
+}
+
+int s3dg_host_parse_devices_env(const char *pin, const char *list, const char *local_rank, const char *world_size,
+                                int ndev, int *out, int cap, int *n) {
     if (!out || !n || cap <= 0) return s3dg_internal_fail(S3DG_EINVAL, "null output");
     *n = 0;
     auto parse_int = [&](const char *&p, int *v) -> bool {
@@ -358,6 +433,14 @@ int s3dg_host_parse_devices(const char *pin, const char *list, int ndev, int *ou
         return S3DG_OK;
     }
     if (ndev <= 0) return s3dg_internal_fail(S3DG_EINVAL, "no GPU visible");
+    // one rank of a multi-process job: its own GPU only
+    int ws = 0, lr = 0;
+    const char *pw = world_size, *pr = local_rank;
+    if (pw && *pw && pr && *pr && parse_int(pw, &ws) && !*pw && ws > 1 && parse_int(pr, &lr) && !*pr) {
+        out[0] = lr % ndev;
+        *n = 1;
+        return S3DG_OK;
+    }
     for (int d = 0; d < ndev && d < cap; ++d) out[(*n)++] = d;
     return S3DG_OK;
 }

@@ -169,6 +169,7 @@ struct HostStaging {
     void *buf[2] = {nullptr, nullptr};
     hipStream_t st[2] = {nullptr, nullptr};
     void *base_user = nullptr;
+    void *pin[2] = {nullptr, nullptr};   // pinned bounce buffers (staged D2H mode only, lazily)
 };
 // What to generate into host memory: the fill_controlled_data / random-data
 // layouts (4 KiB blocks, pp) or DG1 (dgen = true, 1 MiB blocks).

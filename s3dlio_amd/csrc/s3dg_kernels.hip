@@ -238,13 +238,39 @@ __device__ __forceinline__ void patch_image(BlockLds &S, const Plan &P, uint32_t
 }
 
 // Every lane, phase 3: its 16 bytes at byte o of the block: zeros below c, else the image.
+// Diagnostic builds only (tools/variant_lab.py, config-3 A/Bs): S3DG_DIAG_ZERO
+// bit 0 = zero-prefix pieces store the constant S3DG_DIAG_ZVAL instead of 0
+// (same instructions, other data; wrong bytes by design), bit 1 = zero-prefix
+// pieces read their LDS image piece too (same data, the store stream paced
+// like a prefix-free block), bit 2 = a block's pieces stored last-first;
+// S3DG_DIAG_ZPOL = store policy of the zero-prefix pieces (kStore*).
+#ifndef S3DG_DIAG_ZERO
+#define S3DG_DIAG_ZERO 0
+#endif
+#ifndef S3DG_DIAG_ZVAL
+#define S3DG_DIAG_ZVAL 0x5A5A5A5Au
+#endif
 template <int NT>
 __device__ __forceinline__ void write_block(uint8_t *bd, const BlockLds &S, int o) {
     const int c = (int)S.meta[0], L = (int)S.meta[1];
     if (o >= L) return;
+#if S3DG_DIAG_ZERO & 1
+    const u32x4 zero = {S3DG_DIAG_ZVAL, S3DG_DIAG_ZVAL, S3DG_DIAG_ZVAL, S3DG_DIAG_ZVAL};
+#else
     const u32x4 zero = {0u, 0u, 0u, 0u};
+#endif
+#if S3DG_DIAG_ZERO & 2
+    u32x4 im = *reinterpret_cast<const u32x4 *>(S.img + o);
+    asm volatile("" : "+v"(im));
+    const u32x4 v = (o + 16 <= c) ? zero : im;
+#else
     const u32x4 v = (o + 16 <= c) ? zero : *reinterpret_cast<const u32x4 *>(S.img + o);
+#endif
     if (o + 16 <= L) {
+#ifdef S3DG_DIAG_ZPOL
+        if (o + 16 <= c) store16<S3DG_DIAG_ZPOL>(bd + o, v);   // diagnostic: zero pieces' own store policy
+        else
+#endif
         store16<NT>(bd + o, v);
     } else {                                  // ragged object tail: bytes < L only
         const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
@@ -294,8 +320,14 @@ __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, 
         __syncthreads();
     }
 #endif
+#if S3DG_DIAG_ZERO & 4
+    // diagnostic: pieces stored last-first (the zero prefix's stores after the image's)
+#pragma unroll
+    for (int k = SPL - 1; k >= 0; --k) write_block<NT>(bd, S, (int)(t + k * T) * 16);
+#else
 #pragma unroll
     for (int k = 0; k < SPL; ++k) write_block<NT>(bd, S, (int)(t + k * T) * 16);
+#endif
 }
 
 // Stream: blockIdx.x = block (blk_lo + x) of object blockIdx.y of this launch

@@ -355,10 +355,13 @@ def host_context(slot: int = -1) -> Context:
     return Context._borrow(h.value, d.value)
 
 
-def parse_devices(pin: str | None, lst: str | None, ndev: int) -> list[int]:
-    """The slot device list for given env values (pure; s3dg_host_parse_devices)."""
+def parse_devices(pin: str | None, lst: str | None, ndev: int, local_rank: str | None = None,
+                  world_size: str | None = None) -> list[int]:
+    """The slot device list for given env values (pure; s3dg_host_parse_devices_env):
+    S3DLIO_GPU_DEVICE, S3DLIO_GPU_DEVICES, LOCAL_RANK, WORLD_SIZE."""
     out = (ctypes.c_int * 64)()
     n = ctypes.c_int()
-    call("s3dg_host_parse_devices", pin.encode() if pin is not None else None,
-         lst.encode() if lst is not None else None, int(ndev), out, 64, ctypes.byref(n))
+    enc = lambda v: v.encode() if v is not None else None  # noqa: E731
+    call("s3dg_host_parse_devices_env", enc(pin), enc(lst), enc(local_rank), enc(world_size), int(ndev), out, 64,
+         ctypes.byref(n))
     return list(out[:n.value])

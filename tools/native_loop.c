@@ -20,3 +20,55 @@ __attribute__((visibility("default"))) int nl_fill_loop(void *fn, void *ctx, voi
     }
     return 0;
 }
+
+/* The host-buffer drop-in in the criterion shape: `calls` x
+ * s3dlio_fill_controlled_data(buf, len, dedup, compress) on one reused host
+ * buffer (benches/performance_microbenchmarks.rs:43-64). */
+typedef int (*host_fill_fn)(uint8_t *buf, uint64_t len, uint64_t dedup, uint64_t compress);
+
+__attribute__((visibility("default"))) int nl_host_fill_loop(void *fn, void *buf, uint64_t len, uint64_t calls,
+                                                             uint64_t dedup, uint64_t compress) {
+    const host_fill_fn f = (host_fill_fn)fn;
+    for (uint64_t k = 0; k < calls; ++k) {
+        const int r = f((uint8_t *)buf, len, dedup, compress);
+        if (r) return r;
+    }
+    return 0;
+}
+
+/* `threads` threads, each making `calls` s3dg_generate_data(buf_t, len, dedup,
+ * compress, unseeded) calls into its own buffer: generate_into_buffer from 8
+ * Python threads (tests/test_s3dlio_datagen.py:174-204) without the GIL. */
+#include <pthread.h>
+typedef int (*gen_data_fn)(uint8_t *buf, uint64_t size, uint64_t dedup, uint64_t compress, int has_seed,
+                           uint64_t seed);
+typedef struct {
+    gen_data_fn f;
+    uint8_t *buf;
+    uint64_t len, calls, dedup, compress;
+    int rc;
+} nl_job;
+
+static void *nl_thread(void *arg) {
+    nl_job *J = (nl_job *)arg;
+    for (uint64_t k = 0; k < J->calls && !J->rc; ++k) J->rc = J->f(J->buf, J->len, J->dedup, J->compress, 0, 0);
+    return 0;
+}
+
+__attribute__((visibility("default"))) int nl_threads_gen_loop(void *fn, void **bufs, uint64_t len, int threads,
+                                                               uint64_t calls, uint64_t dedup, uint64_t compress) {
+    if (threads < 1 || threads > 64) return -1;
+    nl_job J[64];
+    pthread_t t[64];
+    int started = 0, rc = 0;
+    for (int q = 0; q < threads; ++q) {
+        J[q] = (nl_job){(gen_data_fn)fn, (uint8_t *)bufs[q], len, calls, dedup, compress, 0};
+        if (pthread_create(&t[q], 0, nl_thread, &J[q]) != 0) { rc = -2; break; }
+        ++started;
+    }
+    for (int q = 0; q < started; ++q) {
+        pthread_join(t[q], 0);
+        if (J[q].rc && !rc) rc = J[q].rc;
+    }
+    return rc;
+}

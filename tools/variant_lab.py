@@ -82,9 +82,21 @@ def main():
     sh = ctypes.c_void_p(st.cuda_stream)
     p = ctypes.c_void_p(buf.data_ptr())
 
-    def run(L, h, kind):
+    def stream_params(kind):
         if kind in ("stream2", "stream3", "stream5"):
-            d, fn, fd = {"stream2": (1, 0, 1), "stream3": (4, 1, 2), "stream5": (2, 2, 3)}[kind]
+            return {"stream2": (1, 0, 1), "stream3": (4, 1, 2), "stream5": (2, 2, 3)}[kind]
+        if kind.startswith("sd") and kind.count("x") == 2:   # "sd<dedup>x<f_num>x<f_den>": any stream
+            d, fn, fd = kind[2:].split("x")
+            return int(d), int(fn), int(fd)
+        return None
+
+    for k in os.environ.get("LAB_POINTS", "").split(";"):
+        if stream_params(k.split(":")[0]):
+            work[k.split(":")[0]] = 8 * MiB * n
+
+    def run(L, h, kind):
+        if stream_params(kind):
+            d, fn, fd = stream_params(kind)
             r = L.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(d), u32(fn), u32(fd),
                                               u64(SEED_BASE), u64(0), sh)
         elif kind == "k2":                   # xoshiro keystream, 2 MiB chunks
