@@ -134,6 +134,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")
     p.add_argument("--d2h-reps", type=int, default=1, help="D2H-inclusive samples (diagnosis of run-to-run spread)")
+    p.add_argument("--d2h-full", action="store_true",
+                   help="D2H-inclusive rate over the rank's WHOLE object range (SURVEY 8d: first launch to last "
+                        "D2H completion), instead of an 8 GiB sample; reported beside the device-resident value")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-ceiling", action="store_true")
     p.add_argument("--host-mem", choices=["pageable", "pinned"], default="pageable",
@@ -467,36 +470,43 @@ def main() -> int:
     # ---- D2H-inclusive rate (bounded sample; never `value`) -------------------------------
     d2h = None
     if not args.no_d2h and kind in ("stream", "keystream", "dgen", "dgen_stream"):
-        reps = [d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo) for _ in range(max(1, args.d2h_reps))]
+        cp.barrier()
+        reps = [d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, n_objs=n_rank if args.d2h_full else None)
+                for _ in range(max(1, args.d2h_reps))]
         d2h = reps[-1]
         if len(reps) > 1:
             d2h["all_samples_GiBps"] = [r["value"] for r in reps]
         # every rank measures at the same time: the aggregate is what the node moves
         d2h["aggregate_all_ranks"] = round(cp.sum(d2h["value"]), 2)
+        if args.d2h_full:
+            # whole job: every rank's bytes over the slowest rank's first-launch-to-last-copy time
+            d2h["whole_job_GiBps"] = round(cp.sum(d2h["bytes"]) / cp.max(d2h["seconds"]) / GiB, 2)
+            d2h["verified_vs_oracle"] = bool(cp.max(0.0 if d2h["verified_vs_oracle"] else 1.0) == 0.0)
 
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes)
 
-    if rank == 0 and kind == "host":
-        # the host-buffer path is bound by the PCIe link, not HBM
-        roof = {"bound": "pcie", "achieved": round(achieved_gbs, 1), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved_gbs / PCIE_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
-                "launch_shape": launch_shape, "avg_call_ms": round(avg_ms, 4),
-                "algorithmic_bytes_per_call": algo_per_launch, "host_mem": args.host_mem,
-                "source_digest": source_digest()}
-    elif rank == 0:
-        roof = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic_from_profiles(args.config, algo_per_launch),
-                "kernel": kernel, "launch_shape": launch_shape,
-                "avg_launch_ms": round(avg_ms, 4),
-                "algorithmic_bytes_per_launch": algo_per_launch,
-                "source_digest": source_digest()}
+    if rank == 0:
+        if kind == "host":
+            # the host-buffer path is bound by the PCIe link, not HBM
+            roof = {"bound": "pcie", "achieved": round(achieved_gbs, 1), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved_gbs / PCIE_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
+                    "launch_shape": launch_shape, "avg_call_ms": round(avg_ms, 4),
+                    "algorithmic_bytes_per_call": algo_per_launch, "host_mem": args.host_mem,
+                    "source_digest": source_digest()}
+        else:
+            roof = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                    "traffic": traffic_from_profiles(args.config, algo_per_launch),
+                    "kernel": kernel, "launch_shape": launch_shape,
+                    "avg_launch_ms": round(avg_ms, 4),
+                    "algorithmic_bytes_per_launch": algo_per_launch,
+                    "source_digest": source_digest()}
         if ceil:
             roof.update(ceil)
-            roof["frac_of_write_ceiling"] = round(achieved_gbs / ceil["write_ceiling_GBps"], 4)
+            roof["frac_of_store_only_best"] = round(achieved_gbs / ceil["store_only_best_GBps"], 4)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -643,9 +653,11 @@ def ceilings(torch, ctx, ring, stream, args, store) -> dict:
     def memset_d32(buf, nbytes, stream):
         assert hip.hipMemsetD32Async(buf.data_ptr(), 0x5A5A5A5A, nbytes // 4, int(stream.cuda_stream)) == 0
     shapes["hipMemsetD32Async"] = round(rate(memset_d32), 1)
-    return {"write_ceiling_GBps": fill_ceiling,
-            "write_ceiling_kind": f"k_fill_batch with the PRNG chain and window patches compiled out "
-                                  f"(s3dg_write_ceiling_fill), 8 MiB objects, best pacing {best_pace}",
+    # not a ceiling: the fill runs above every store-only shape
+    return {"store_only_best_GBps": fill_ceiling,
+            "store_only_best_kind": f"k_fill_batch with the PRNG chain and window patches compiled out "
+                                    f"(s3dg_write_ceiling_fill), 8 MiB objects, best pacing {best_pace}; "
+                                    f"a reference shape, not a bound: the fill writes faster (DESIGN.md §5.1.1)",
             "store_only_shapes_GBps": shapes}
 
 
@@ -679,18 +691,30 @@ def numa_of(ptr: int) -> dict:
     return {k: int(v) for k, v in (f.split("=") for f in line.split() if f[:1] == "N" and "=" in f)}
 
 
-def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=256 * MiB):
-    """Generate `total` bytes of the config's objects through two device chunk
-    buffers and copy each chunk to a pinned host ring on the GPU's NUMA node,
-    on a second stream (the PUT path's input).  Logs where the ring's pages
-    are, the CPUs the process runs on and the per-copy rates (HIP events on
-    the copy stream), so run-to-run spread can be attributed."""
+def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=256 * MiB, n_objs=None):
+    """Generate the config's objects through two device chunk buffers and
+    copy each chunk to a pinned host ring on the GPU's NUMA node, on a second
+    stream (the PUT path's input).  Default: an 8 GiB sample.  n_objs (the
+    --d2h-full mode): all of the rank's objects [lo, lo + n_objs),
+    timed from the first launch to the last D2H completion, the last host
+    chunk checked against the oracle.  Logs where the ring's pages are, the
+    CPUs the process runs on and the per-copy rates (HIP events on the copy
+    stream), so run-to-run spread can be attributed."""
     kind = cfg["kind"]
     size = cfg["size"]
     dg = kind in ("dgen", "dgen_stream")
     per_chunk = max(1, chunk // size) if not dg else 1
     cb = per_chunk * size if not dg else chunk
-    nchunks = total // cb
+    if n_objs is None:
+        nchunks = total // cb
+        chunk_objs = [per_chunk] * nchunks
+    elif dg:             # DG1: the objects' 1 MiB blocks, chunk by chunk
+        tot = n_objs * size
+        nchunks = (tot + cb - 1) // cb
+        chunk_objs = [1] * nchunks
+    else:
+        nchunks = (n_objs + per_chunk - 1) // per_chunk
+        chunk_objs = [min(per_chunk, n_objs - k * per_chunk) for k in range(nchunks)]
     gen = torch.cuda.Stream(device=dev)
     cpy = torch.cuda.Stream(device=dev)
     devbuf = [torch.empty(cb, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(2)]
@@ -704,44 +728,69 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
     gen_done = [torch.cuda.Event() for _ in range(2)]
     cpy_done = [torch.cuda.Event() for _ in range(2)]
     cev = []
+    blocks_per_obj = (size + MiB - 1) // MiB if dg else 0
+
+    def chunk_bytes(k):
+        if dg:
+            if n_objs is None:
+                return cb
+            return min(cb, n_objs * size - k * cb)
+        return chunk_objs[k] * size
 
     def run(n, timed):
         for k in range(n):
             s = k & 1
+            nb = chunk_bytes(k)
             gen.wait_event(cpy_done[s])
             if kind == "keystream":
-                call("s3dg_xoshiro_fill", ctx._h, int(devbuf[s].data_ptr()), cb, 2 * MiB,
+                call("s3dg_xoshiro_fill", ctx._h, int(devbuf[s].data_ptr()), nb, 2 * MiB,
                      (lo * size + k * cb) // (2 * MiB), int(gen.cuda_stream))
-            elif kind in ("dgen", "dgen_stream"):
-                call("s3dg_dgen_fill", ctx._h, int(devbuf[s].data_ptr()), size, k * (cb >> 20),
-                     (k + 1) * (cb >> 20), cfg["dedup"], fn, fd, SEED_BASE, int(gen.cuda_stream))
+            elif dg:
+                # chunk k = MiB blocks [k*cb, k*cb + nb) of the objects laid end to end
+                b0 = k * (cb >> 20)
+                j, blk = divmod(b0, blocks_per_obj)
+                call("s3dg_dgen_fill", ctx._h, int(devbuf[s].data_ptr()), size, blk, blk + (nb >> 20),
+                     cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, lo + j) if n_objs is not None else SEED_BASE,
+                     int(gen.cuda_stream))
             else:
                 call("s3dg_fill_controlled_stream", ctx._h, int(devbuf[s].data_ptr()), size, size,
-                     per_chunk, cfg["dedup"], fn, fd, SEED_BASE, lo + k * per_chunk, int(gen.cuda_stream))
+                     chunk_objs[k], cfg["dedup"], fn, fd, SEED_BASE, lo + k * per_chunk, int(gen.cuda_stream))
             gen_done[s].record(gen)
             cpy.wait_event(gen_done[s])
             if timed:
                 cev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 cev[-1][0].record(cpy)
-            call("s3dg_d2h_async", ctx._h, host[s], int(devbuf[s].data_ptr()), cb, int(cpy.cuda_stream))
+            call("s3dg_d2h_async", ctx._h, host[s], int(devbuf[s].data_ptr()), nb, int(cpy.cuda_stream))
             if timed:
                 cev[-1][1].record(cpy)
             cpy_done[s].record(cpy)
+    verified = None
     try:
         for s in range(2):
             cpy_done[s].record(cpy)
-        run(max(2, nchunks // 4), False)          # the first GiBs into fresh pinned pages copy slower
+        # the first GiBs into fresh pinned pages copy slower
+        run(max(2, nchunks // 4) if n_objs is None else min(4, nchunks), False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run(nchunks, True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         pages = [numa_of(p) for p in host]
+        if n_objs is not None and kind == "stream":
+            # the last chunk's first object, from pinned host memory, vs the oracle
+            import numpy as np
+            from oracle import oracle_c as OC
+            k = nchunks - 1
+            got = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(host[k & 1]))
+            exp = OC.fill_controlled(size, cfg["dedup"], fn, fd, object_entropy_py(SEED_BASE, lo + k * per_chunk),
+                                     OC.base_block(BASE_SEED))
+            verified = bool(np.array_equal(got, exp))
     finally:
         torch.cuda.synchronize()
         for p in host:
             call("s3dg_host_free_pinned", p)
-    rates = sorted(cb / (a.elapsed_time(b) * 1e-3) / GiB for a, b in cev)
+    done_bytes = sum(chunk_bytes(k) for k in range(nchunks))
+    rates = sorted(chunk_bytes(k) / (a.elapsed_time(b) * 1e-3) / GiB for k, (a, b) in enumerate(cev))
     cpus = sorted(os.sched_getaffinity(0))
     cpu_nodes = set()
     for nd in os.listdir("/sys/devices/system/node") if os.path.isdir("/sys/devices/system/node") else []:
@@ -756,13 +805,20 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
                     cpu_nodes.add(int(nd[4:]))
             except Exception:
                 pass
-    return {"value": round(nchunks * cb / dt / GiB, 2), "unit": "GiB/s",
-            "sample": f"{nchunks} x {cb // MiB} MiB device chunks ({nchunks * cb // GiB} GiB) of the config's "
-                      f"objects, 2 device chunks, pinned host ring (hipHostMalloc default flags, allocated from a "
-                      f"thread bound to the GPU's local CPUs), generate || D2H on two streams",
-            "gpu_numa_node": node.value, "ring_pages_per_node": pages,
-            "process_cpu_nodes": sorted(cpu_nodes),
-            "copy_GiBps_min_med_max": [round(rates[0], 1), round(rates[len(rates) // 2], 1), round(rates[-1], 1)]}
+    what = (f"the rank's whole object range ({n_objs} objects, {done_bytes / 1e9:.1f} GB), first launch to last "
+            f"D2H completion" if n_objs is not None else f"{nchunks} x {cb // MiB} MiB device chunks "
+            f"({done_bytes // GiB} GiB) of the config's objects")
+    out = {"value": round(done_bytes / dt / GiB, 2), "unit": "GiB/s",
+           "mode": "full" if n_objs is not None else "sample",
+           "bytes": done_bytes, "seconds": round(dt, 4),
+           "sample": f"{what}, 2 device chunks of {cb // MiB} MiB, pinned host ring (hipHostMalloc default flags, "
+                     f"allocated from a thread bound to the GPU's local CPUs), generate || D2H on two streams",
+           "gpu_numa_node": node.value, "ring_pages_per_node": pages,
+           "process_cpu_nodes": sorted(cpu_nodes),
+           "copy_GiBps_min_med_max": [round(rates[0], 1), round(rates[len(rates) // 2], 1), round(rates[-1], 1)]}
+    if n_objs is not None:
+        out["verified_vs_oracle"] = verified
+    return out
 
 
 def object_entropy_py(seed_base: int, j: int) -> int:

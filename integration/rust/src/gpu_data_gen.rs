@@ -4,25 +4,29 @@
 // behind s3dlio's own data-generation API.
 //
 // A REFERENCE PATCH: cargo/rustc are not in this build's image, so this file is
-// not compiled here.  Every extern "C" call below is exercised, in the same
-// order and with the same arguments, by tests/capi/binding_abi.c (built and run
-// by tests/test_capi_binding.py), which is the tested form of this binding.
+// not compiled here.  Every extern "C" call below is made, with the same
+// arguments, by tests/capi/binding_abi.c (built and run by
+// tests/test_capi_binding.py), which is the tested form of this binding.
 //
-// Public signatures are exactly the reference's (paths relative to the s3dlio
-// checkout):
-//   fill_controlled_data                 src/data_gen.rs:151
-//   generate_random_data                 src/data_gen.rs:102
-//   generate_object                      src/data_gen.rs:29
-//   generate_controlled_data_streaming   src/data_gen.rs:232
-//   DataGenerator / ObjectGen            src/data_gen.rs:253-371
-//   generate_controlled_data_alt         src/data_gen_alt.rs:66
-//   ObjectGenAlt                         src/data_gen_alt.rs:89-149
-//   generate_npz_bytes_raw               src/data_formats/npz.rs:322 (behind the
-//                                        PyO3 generate_npz_bytes, python_datagen_api.rs:395)
-// The reference functions are infallible except generate_object and
-// generate_npz_bytes_raw; here a GPU or HIP failure is a configuration error,
-// so the infallible ones panic with the library's message (the reference would
-// have no GPU path to fail).
+// What it replaces (paths relative to the s3dlio checkout):
+//   * the in-tree generators of src/data_gen.rs, same signatures:
+//       fill_controlled_data (:151), generate_random_data (:102),
+//       generate_object (:29); plus the seeded sibling SURVEY §8b asks for;
+//   * the dgen-data 0.2.4 items src/data_gen_alt.rs:14-16 re-exports:
+//       generate_data, generate_data_simple, DataBuffer, DataGenerator,
+//       GeneratorConfig, NumaMode (the `dgen` section below);
+//   * generate_npz_bytes_raw (src/data_formats/npz.rs:322).
+// What it leaves alone: data_gen.rs's DataGenerator / ObjectGen /
+// generate_controlled_data_streaming (:232-371) and data_gen_alt.rs's
+// ObjectGenAlt / generate_controlled_data_alt / generate_data_with_config
+// (:56-149).  They only call the re-exported dgen items, so re-pointing the
+// re-export moves them onto the GPU unchanged.
+//
+// Errors: the reference's infallible functions panic with the library's
+// message (a GPU or HIP failure is a configuration error the CPU code cannot
+// have); generate_object and generate_npz_bytes_raw return anyhow errors as the
+// reference does; the try_* forms return them for the PyO3 layer
+// (python_api/python_datagen_api_gpu.rs), which raises RuntimeError.
 
 use std::ffi::{c_char, c_int, CStr, CString};
 
@@ -77,13 +81,19 @@ fn last_error() -> String {
     unsafe { CStr::from_ptr(s3dg_last_error()).to_string_lossy().into_owned() }
 }
 
-fn ok_or_panic(rc: c_int) {
-    assert!(rc == 0, "s3dlio_amd: {}", last_error());
+fn check(rc: c_int) -> anyhow::Result<()> {
+    if rc == 0 { Ok(()) } else { anyhow::bail!("s3dlio_amd: {}", last_error()) }
 }
 
-// ---- src/data_gen.rs ---------------------------------------------------------
+fn ok_or_panic(rc: c_int) {
+    if let Err(e) = check(rc) {
+        panic!("{e}");
+    }
+}
 
-/// `fill_controlled_data` (src/data_gen.rs:151): same signature, same byte
+// ---- src/data_gen.rs (in-tree generators) ---------------------------------------
+
+/// `fill_controlled_data` (src/data_gen.rs:151): same signature and byte
 /// layout for a given entropy and base block; time entropy and a per-process
 /// random A_BASE_BLOCK as the reference.  Generated on the GPUs (host slots)
 /// and copied into `buf`; the Rayon `install()` context has no meaning here.
@@ -102,8 +112,7 @@ pub fn fill_controlled_data_seeded(buf: &mut [u8], dedup: usize, compress: usize
         return Ok(());
     }
     let p = base.map_or(std::ptr::null(), |b| b.as_ptr());
-    let rc = unsafe { s3dlio_fill_controlled_data_seeded(buf.as_mut_ptr(), buf.len(), dedup, compress, entropy, p) };
-    if rc == 0 { Ok(()) } else { anyhow::bail!("s3dlio_amd: {}", last_error()) }
+    check(unsafe { s3dlio_fill_controlled_data_seeded(buf.as_mut_ptr(), buf.len(), dedup, compress, entropy, p) })
 }
 
 /// `generate_random_data` (src/data_gen.rs:102): BASE_BLOCK tiled, the first
@@ -127,177 +136,185 @@ fn object_type_code(t: &ObjectType) -> c_int {
 }
 
 /// `generate_object` (src/data_gen.rs:29): payload (random layout, or the
-/// dgen-contract stream when `use_controlled`) framed as the object type.
-/// HDF5 is an error, as a reference build without the `hdf5` feature.
+/// dgen-contract stream when `use_controlled`) generated straight into its
+/// place in the framed object (no `.to_vec()` / `build_raw` copies).  HDF5 is
+/// an error, as a reference build without the `hdf5` feature.
 pub fn generate_object(cfg: &Config) -> anyhow::Result<bytes::Bytes> {
     let t = object_type_code(&cfg.object_type);
     let mut need = 0u64;
-    if unsafe { s3dg_object_size(t, cfg.elements as u64, cfg.element_size as u64, &mut need) } != 0 {
-        anyhow::bail!("{}", last_error());
-    }
+    check(unsafe { s3dg_object_size(t, cfg.elements as u64, cfg.element_size as u64, &mut need) })?;
     let mut out = vec![0u8; need as usize];
     let mut written = 0u64;
     let mode = match cfg.data_gen_mode {
         DataGenMode::Streaming => S3DG_MODE_STREAMING,
         DataGenMode::SinglePass => S3DG_MODE_SINGLE_PASS,
     };
-    let rc = unsafe {
+    check(unsafe {
         s3dg_generate_object(t, cfg.elements as u64, cfg.element_size as u64, cfg.use_controlled as c_int,
                              cfg.dedup_factor as u64, cfg.compress_factor as u64, mode, 0, 0,
                              out.as_mut_ptr(), need, &mut written)
-    };
-    if rc != 0 {
-        anyhow::bail!("{}", last_error());
-    }
+    })?;
     out.truncate(written as usize);
     Ok(bytes::Bytes::from(out))
 }
 
-/// `generate_controlled_data_streaming` (src/data_gen.rs:232).  Generation
-/// is positional, so the chunk size changes nothing but the copy granularity.
-pub fn generate_controlled_data_streaming(size: usize, dedup: usize, compress: usize,
-                                          chunk_size: usize) -> Vec<u8> {
-    let gen = DataGenerator::new(None);
-    let mut object_gen = gen.begin_object(size, dedup, compress);
-    let mut result = Vec::with_capacity(size);
-    while !object_gen.is_complete() {
-        match object_gen.fill_chunk(chunk_size) {
-            Some(chunk) => result.extend_from_slice(&chunk),
-            None => break,
-        }
-    }
-    result
+// ---- dgen: the dgen-data 0.2.4 surface src/data_gen_alt.rs:14-16 re-exports ----
+//
+// dgen-data's own bytes are unknown here (the crate is absent: parity unpinned);
+// these items generate the build-defined DG1 layout, which
+// meets the statistical contract the reference's tests pin (SURVEY Appendix
+// B).  Under the `gpu` feature src/data_gen_alt.rs:14-16 becomes
+//     pub use crate::gpu_data_gen::{generate_data, generate_data_simple, DataBuffer,
+//                                   DataGenerator, GeneratorConfig, NumaMode};
+// and src/python_api/python_datagen_api.rs is replaced by
+// python_api/python_datagen_api_gpu.rs.
+
+/// `dgen_data::NumaMode`.  Accepted for source compatibility: generation runs
+/// on the GPUs' HBM, the host buffer is the caller's.
+#[derive(Clone, Copy, Debug, Default, PartialEq, Eq)]
+pub enum NumaMode {
+    #[default]
+    Auto,
+    Force,
+    Disabled,
 }
 
-/// `DataGenerator` (src/data_gen.rs:253-305): an instance entropy, explicit or
-/// time + thread-local counter (:271-291); every object begun from it is seeded
-/// with that entropy, so repeated `begin_object` calls give identical objects.
-pub struct DataGenerator {
-    instance_entropy: u64,
+/// `dgen_data::GeneratorConfig` (field list as built at
+/// src/python_api/python_datagen_api.rs:59-68).  `max_threads`, `numa_mode` and
+/// `numa_node` size the CPU pool of the reference and are ignored here;
+/// `block_size` must be None or 1 MiB (DG1's dedup unit, src/constants.rs:348).
+#[derive(Clone, Debug)]
+pub struct GeneratorConfig {
+    pub size: usize,
+    pub dedup_factor: usize,
+    pub compress_factor: usize,
+    pub numa_mode: NumaMode,
+    pub max_threads: Option<usize>,
+    pub numa_node: Option<usize>,
+    pub block_size: Option<usize>,
+    pub seed: Option<u64>,
 }
 
-impl DataGenerator {
-    pub fn new(seed: Option<u64>) -> Self {
-        let instance_entropy = match seed {
-            Some(s) => s,
-            None => {
-                use std::cell::Cell;
-                use std::time::{SystemTime, UNIX_EPOCH};
-                thread_local! {
-                    static ENTROPY_COUNTER: Cell<u64> = const { Cell::new(0) };
-                }
-                let base = SystemTime::now().duration_since(UNIX_EPOCH).unwrap_or_default().as_nanos() as u64;
-                let counter = ENTROPY_COUNTER.with(|c| {
-                    let v = c.get();
-                    c.set(v.wrapping_add(1));
-                    v
-                });
-                base.wrapping_add(counter)
-            }
-        };
-        Self { instance_entropy }
-    }
-
-    pub fn new_with_seed(seed: u64) -> Self {
-        Self::new(Some(seed))
-    }
-
-    pub fn begin_object(&self, size: usize, dedup: usize, compress: usize) -> ObjectGen {
-        ObjectGen { alt_gen: ObjectGenAlt::new_with_seed(size, dedup, compress, self.instance_entropy) }
-    }
-}
-
-impl Default for DataGenerator {
+impl Default for GeneratorConfig {
     fn default() -> Self {
-        Self::new(None)
+        Self { size: 0, dedup_factor: 1, compress_factor: 1, numa_mode: NumaMode::Auto, max_threads: None,
+               numa_node: None, block_size: None, seed: None }
     }
 }
 
-/// `ObjectGen` (src/data_gen.rs:308-371).
-pub struct ObjectGen {
-    alt_gen: ObjectGenAlt,
-}
+const DGEN_BLOCK: usize = 1 << 20;
 
-impl ObjectGen {
-    pub fn fill_chunk(&mut self, chunk_size: usize) -> Option<Vec<u8>> {
-        assert!(chunk_size > 0, "Chunk size must be greater than 0"); // :328
-        let mut buf = vec![0u8; chunk_size];
-        let written = self.alt_gen.fill_chunk(&mut buf);
-        if written == 0 {
-            return None;
-        }
-        buf.truncate(written);
-        Some(buf)
-    }
-    pub fn is_complete(&self) -> bool {
-        self.alt_gen.is_complete()
-    }
-    pub fn reset(&mut self) {
-        self.alt_gen.reset()
-    }
-    pub fn position(&self) -> usize {
-        self.alt_gen.position()
-    }
-    pub fn total_size(&self) -> usize {
-        self.alt_gen.total_size()
-    }
-    pub fn fill_remaining(&mut self) -> Vec<u8> {
-        const CHUNK: usize = 32 * 1024 * 1024; // :360
-        let mut result = Vec::with_capacity(self.total_size().saturating_sub(self.position()));
-        while !self.is_complete() {
-            match self.fill_chunk(CHUNK) {
-                Some(c) => result.extend_from_slice(&c),
-                None => break,
-            }
-        }
-        result
+fn check_block_size(cfg: &GeneratorConfig) -> anyhow::Result<()> {
+    match cfg.block_size {
+        None | Some(DGEN_BLOCK) => Ok(()),
+        Some(b) => anyhow::bail!("s3dlio_amd: block_size {b} unsupported (DG1 uses 1 MiB blocks)"),
     }
 }
 
-// ---- src/data_gen_alt.rs -----------------------------------------------------
-
-/// `generate_controlled_data_alt` (src/data_gen_alt.rs:66): `.max(1)` on dedup
-/// and compress; seeded output is reproducible.
-pub fn generate_controlled_data_alt(size: usize, dedup: usize, compress: usize,
-                                    seed: Option<u64>) -> bytes::Bytes {
-    let mut v = vec![0u8; size];
-    if size > 0 {
-        ok_or_panic(unsafe {
-            s3dg_generate_data(v.as_mut_ptr(), size as u64, dedup.max(1) as u64, compress.max(1) as u64,
-                               seed.is_some() as c_int, seed.unwrap_or(0))
-        });
-    }
-    bytes::Bytes::from(v)
+/// `dgen_data::DataBuffer`: the owned result of `generate_data`.
+pub struct DataBuffer {
+    data: Vec<u8>,
 }
 
-/// `ObjectGenAlt` (src/data_gen_alt.rs:89-149) over the library's streaming
-/// generator (s3dg_gen_*): one host slot (GPU) per generator.
-pub struct ObjectGenAlt {
+impl DataBuffer {
+    pub fn as_slice(&self) -> &[u8] {
+        &self.data
+    }
+    pub fn as_mut_slice(&mut self) -> &mut [u8] {
+        &mut self.data
+    }
+    pub fn as_ptr(&self) -> *const u8 {
+        self.data.as_ptr()
+    }
+    pub fn len(&self) -> usize {
+        self.data.len()
+    }
+    pub fn is_empty(&self) -> bool {
+        self.data.is_empty()
+    }
+    /// Zero-copy hand-off (`Bytes::from(Vec)`), as src/data_gen_alt.rs:57 uses it.
+    pub fn into_bytes(self) -> bytes::Bytes {
+        bytes::Bytes::from(self.data)
+    }
+}
+
+/// Fill `buf` in place with a DG1 object of `buf.len()` bytes; `seed` None =
+/// time + per-process counter.  The zero-copy write behind the PyO3
+/// `generate_into_buffer` (no intermediate DataBuffer, unlike
+/// python_datagen_api.rs:179-197).
+pub fn try_generate_into(buf: &mut [u8], dedup: usize, compress: usize, seed: Option<u64>) -> anyhow::Result<()> {
+    if buf.is_empty() {
+        return Ok(());
+    }
+    check(unsafe {
+        s3dg_generate_data(buf.as_mut_ptr(), buf.len() as u64, dedup as u64, compress as u64,
+                           seed.is_some() as c_int, seed.unwrap_or(0))
+    })
+}
+
+/// `dgen_data::generate_data`, fallible form.  Unlike dgen's batch path
+/// (src/data_gen_alt.rs:63-64) the seed is honoured, as the reference's tests
+/// expect (tests/test_high_speed_data_gen.rs:148-198).
+pub fn try_generate_data(config: GeneratorConfig) -> anyhow::Result<DataBuffer> {
+    check_block_size(&config)?;
+    let mut data = vec![0u8; config.size];
+    try_generate_into(&mut data, config.dedup_factor, config.compress_factor, config.seed)?;
+    Ok(DataBuffer { data })
+}
+
+/// `dgen_data::generate_data(GeneratorConfig) -> DataBuffer`.
+pub fn generate_data(config: GeneratorConfig) -> DataBuffer {
+    try_generate_data(config).unwrap_or_else(|e| panic!("{e}"))
+}
+
+/// `dgen_data::generate_data_simple(size, dedup, compress)`.
+pub fn generate_data_simple(size: usize, dedup: usize, compress: usize) -> DataBuffer {
+    generate_data(GeneratorConfig { size, dedup_factor: dedup, compress_factor: compress, ..Default::default() })
+}
+
+/// `generate_data_with_config` (src/data_gen_alt.rs:56-58), for callers that
+/// import it from here; data_gen_alt.rs's own copy works unchanged over the
+/// re-exported items.
+pub fn generate_data_with_config(config: GeneratorConfig) -> bytes::Bytes {
+    generate_data(config).into_bytes()
+}
+
+/// `dgen_data::DataGenerator`: one object's positional stream over the
+/// library's generator handle (s3dg_gen_*), on one host slot (GPU).  Output
+/// does not depend on the chunk sizes passed to `fill_chunk`.
+pub struct DataGenerator {
     g: *mut S3dgGen,
 }
 
-// the library serialises calls on one generator; a generator may move threads
-unsafe impl Send for ObjectGenAlt {}
+// The library serialises calls on one handle; a generator may move threads
+// (the PyO3 Generator calls it under py.detach).
+unsafe impl Send for DataGenerator {}
 
-impl ObjectGenAlt {
-    pub fn new(total_size: usize, dedup: usize, compress: usize) -> Self {
-        Self::create(total_size, dedup, compress, None)
-    }
-    pub fn new_with_seed(total_size: usize, dedup: usize, compress: usize, seed: u64) -> Self {
-        Self::create(total_size, dedup, compress, Some(seed))
-    }
-    fn create(total_size: usize, dedup: usize, compress: usize, seed: Option<u64>) -> Self {
+impl DataGenerator {
+    pub fn try_new(config: GeneratorConfig) -> anyhow::Result<Self> {
+        check_block_size(&config)?;
         let mut g = std::ptr::null_mut();
-        ok_or_panic(unsafe {
-            s3dg_gen_create(total_size as u64, dedup.max(1) as u64, compress.max(1) as u64,
-                            seed.is_some() as c_int, seed.unwrap_or(0), &mut g)
-        });
-        Self { g }
+        check(unsafe {
+            s3dg_gen_create(config.size as u64, config.dedup_factor as u64, config.compress_factor as u64,
+                            config.seed.is_some() as c_int, config.seed.unwrap_or(0), &mut g)
+        })?;
+        Ok(Self { g })
     }
-    pub fn fill_chunk(&mut self, buf: &mut [u8]) -> usize {
+    pub fn new(config: GeneratorConfig) -> Self {
+        Self::try_new(config).unwrap_or_else(|e| panic!("{e}"))
+    }
+    /// Chunk size the PyO3 `Generator` defaults to (python_datagen_api.rs:285).
+    pub fn recommended_chunk_size() -> usize {
+        32 << 20
+    }
+    pub fn try_fill_chunk(&mut self, buf: &mut [u8]) -> anyhow::Result<usize> {
         let mut w = 0u64;
-        ok_or_panic(unsafe { s3dg_gen_fill_chunk(self.g, buf.as_mut_ptr(), buf.len() as u64, &mut w) });
-        w as usize
+        check(unsafe { s3dg_gen_fill_chunk(self.g, buf.as_mut_ptr(), buf.len() as u64, &mut w) })?;
+        Ok(w as usize)
+    }
+    /// Next bytes of the object into `buf`; returns the count (0 when complete).
+    pub fn fill_chunk(&mut self, buf: &mut [u8]) -> usize {
+        self.try_fill_chunk(buf).unwrap_or_else(|e| panic!("{e}"))
     }
     pub fn is_complete(&self) -> bool {
         unsafe { s3dg_gen_is_complete(self.g) != 0 }
@@ -313,7 +330,7 @@ impl ObjectGenAlt {
     }
 }
 
-impl Drop for ObjectGenAlt {
+impl Drop for DataGenerator {
     fn drop(&mut self) {
         unsafe {
             s3dg_gen_destroy(self.g);
@@ -329,20 +346,13 @@ pub fn generate_npz_bytes_raw(shape: &[usize], dtype_str: &str, num_samples: usi
     let dims: Vec<u64> = shape.iter().map(|&d| d as u64).collect();
     let dt = CString::new(dtype_str)?;
     let mut total = 0u64;
-    if unsafe { s3dg_npz_size(dims.as_ptr(), dims.len() as c_int, dt.as_ptr(), num_samples as u64, &mut total) } != 0 {
-        anyhow::bail!("{}", last_error());
-    }
+    check(unsafe { s3dg_npz_size(dims.as_ptr(), dims.len() as c_int, dt.as_ptr(), num_samples as u64, &mut total) })?;
     let mut ctx = std::ptr::null_mut();
-    if unsafe { s3dg_host_slot_context(-1, &mut ctx) } != 0 {
-        anyhow::bail!("{}", last_error());
-    }
+    check(unsafe { s3dg_host_slot_context(-1, &mut ctx) })?;
     let mut out = vec![0u8; total as usize];
-    let rc = unsafe {
+    check(unsafe {
         s3dg_npz_build(ctx, dims.as_ptr(), dims.len() as c_int, dt.as_ptr(), num_samples as u64,
                        out.as_mut_ptr(), total)
-    };
-    if rc != 0 {
-        anyhow::bail!("{}", last_error());
-    }
+    })?;
     Ok(out)
 }

@@ -144,7 +144,8 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
             std::mutex mu;
             void *dev = nullptr;
             uint64_t cap = 0;
-            hipStream_t s = nullptr;
+            hipStream_t s = nullptr, s_crc = nullptr;   // D2H stream, CRC stream
+            hipEvent_t filled = nullptr;
         };
         static std::mutex map_mu;
         static std::map<int, Cache *> *caches = new std::map<int, Cache *>();   // never freed: outlives HIP
@@ -165,6 +166,10 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
         hipStream_t &s = C->s;
         if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
             return s3dg_internal_fail(S3DG_EHIP, "hipStreamCreate");
+        if (!C->s_crc && hipStreamCreateWithFlags(&C->s_crc, hipStreamNonBlocking) != hipSuccess)
+            return s3dg_internal_fail(S3DG_EHIP, "hipStreamCreate");
+        if (!C->filled && hipEventCreateWithFlags(&C->filled, hipEventDisableTiming) != hipSuccess)
+            return s3dg_internal_fail(S3DG_EHIP, "hipEventCreate");
         if (L.x_data > cap) {
             if (dev) (void)hipFree(dev);
             dev = nullptr;
@@ -175,12 +180,17 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
         }
         uint32_t cd = 0;
         if (int r = s3dg_xoshiro_fill(ctx, dev, L.x_data, 2u << 20, 0, s)) return r;   // :376-383
-        // D2H, then the CRC kernel (stream order; both only read the keystream)
+        // The D2H (PCIe) and the CRC kernel (HBM reads) both only read the
+        // keystream: the CRC runs on a second stream, hidden under the copy.
+        if (hipEventRecord(C->filled, s) != hipSuccess || hipStreamWaitEvent(C->s_crc, C->filled, 0) != hipSuccess)
+            return s3dg_internal_fail(S3DG_EHIP, "npz event");
         if (hipMemcpyAsync(out + L.off_x_data, dev, L.x_data, hipMemcpyDeviceToHost, s) != hipSuccess)
             return s3dg_internal_fail(S3DG_EHIP, "npz x-data D2H");
-        if (int r = s3dg_internal_crc_device(ctx, dev, L.x_data, s, &cd)) return r;
+        const int rc = s3dg_internal_crc_device(ctx, dev, L.x_data, C->s_crc, &cd);   // waits for s_crc only
+        const hipError_t es = hipStreamSynchronize(s);
+        if (rc) return rc;
+        if (es != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, "npz sync");
         crc_x = crc32_combine(crc_x, cd, L.x_data);                                    // :386
-        if (hipStreamSynchronize(s) != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, "npz sync");
     }
     // x.npy: local header + NPY header (:368-372, patched :389-392)
     local_header(out, "x.npy", crc_x, (uint32_t)L.x_npy);

@@ -139,6 +139,75 @@ int main(int argc, char **argv) {
                                          memcmp(a, b, n) != 0);
         free(a); free(b);
     }
+    /* dgen surface re-exported by src/data_gen_alt.rs:14-16: generate_data
+       (GeneratorConfig, seed honoured), generate_data_simple, DataBuffer */
+    {
+        const uint64_t n = 3 * MiB + 333;
+        uint8_t *a = xalloc(n), *b = xalloc(n), *c = xalloc(n);
+        CHECK("dgen generate_data(config{seed})", s3dg_generate_data(a, n, 2, 2, 1, 0xDEADBEEF) == 0 &&
+                                                      s3dg_generate_data(b, n, 2, 2, 1, 0xDEADBEEF) == 0);
+        CHECK("dgen generate_data: same seed, same bytes", memcmp(a, b, n) == 0);
+        s3dgo_dgen_fill(c, n, 2, 1, 2, 0xDEADBEEF);
+        CHECK("dgen generate_data == DG1 oracle", memcmp(a, c, n) == 0);
+        CHECK("dgen generate_data: other seed differs",
+              s3dg_generate_data(b, n, 2, 2, 1, 0x12345678) == 0 && memcmp(a, b, n) != 0);
+        CHECK("dgen generate_data_simple", s3dg_generate_data(a, n, 1, 1, 0, 0) == 0 &&
+                                               s3dg_generate_data(b, n, 1, 1, 0, 0) == 0 && memcmp(a, b, n) != 0);
+        CHECK("dgen generate_data_simple(0 bytes)", s3dg_generate_data(a, 0, 1, 1, 0, 0) == 0);
+        free(a); free(b); free(c);
+    }
+    /* dgen DataGenerator::new(config) with the recommended 32 MiB chunk (the
+       PyO3 Generator's default, python_datagen_api.rs:308) */
+    {
+        const uint64_t n = 40 * MiB + 5, chunk = 32 * MiB;
+        s3dg_gen *g = NULL;
+        CHECK("dgen DataGenerator::new", s3dg_gen_create(n, 1, 3, 1, 31337, &g) == 0);
+        uint8_t *a = xalloc(n), *b = xalloc(n);
+        uint64_t w1 = 0, w2 = 0, w3 = 0;
+        CHECK("dgen DataGenerator::fill_chunk x2", s3dg_gen_fill_chunk(g, a, chunk, &w1) == 0 && w1 == chunk &&
+                                                      s3dg_gen_fill_chunk(g, a + w1, chunk, &w2) == 0 &&
+                                                      w2 == n - chunk);
+        CHECK("dgen DataGenerator: complete, then 0", s3dg_gen_is_complete(g) && s3dg_gen_fill_chunk(g, b, 8, &w3) == 0 &&
+                                                         w3 == 0 && s3dg_gen_position(g) == n);
+        s3dgo_dgen_fill(b, n, 1, 2, 3, 31337);
+        CHECK("dgen DataGenerator == DG1 oracle", memcmp(a, b, n) == 0);
+        s3dg_gen_destroy(g);
+        free(a); free(b);
+    }
+    /* PyO3 generate_into_buffer (python_datagen_api.rs:150): straight into the
+       caller's buffer, exactly its bytes (guards around it stay) */
+    {
+        const uint64_t n = 5 * MiB + 77, pad = 4096;
+        uint8_t *a = xalloc(n + 2 * pad);
+        memset(a, 0xAB, n + 2 * pad);
+        CHECK("PyO3 generate_into_buffer", s3dg_generate_data(a + pad, n, 4, 2, 0, 0) == 0);
+        int guards = 1;
+        for (uint64_t k = 0; k < pad; ++k) guards &= a[k] == 0xAB && a[pad + n + k] == 0xAB;
+        CHECK("PyO3 generate_into_buffer: guards intact", guards);
+        uint64_t zeros = 0;
+        for (uint64_t k = 0; k < n; ++k) zeros += a[pad + k] == 0;
+        CHECK("PyO3 generate_into_buffer: zero fraction ~ (c-1)/c", zeros > n * 45 / 100 && zeros < n * 55 / 100);
+        free(a);
+    }
+    /* PyO3 Generator(size, dedup, compress, threads, chunk_size, seed) and
+       generate_data / generate_data_with_threads (python_datagen_api.rs:49-123,
+       :270-365): a seeded generator, a buffer larger than what is left */
+    {
+        const uint64_t n = 2 * MiB + 1;
+        s3dg_gen *g = NULL;
+        CHECK("PyO3 Generator(seed)", s3dg_gen_create(n, 2, 1, 1, 4242, &g) == 0);
+        uint8_t *a = xalloc(4 * MiB), *b = xalloc(n);
+        uint64_t w = 0;
+        CHECK("PyO3 Generator.fill_chunk(bigger buffer)", s3dg_gen_fill_chunk(g, a, 4 * MiB, &w) == 0 && w == n);
+        s3dgo_dgen_fill(b, n, 2, 0, 1, 4242);
+        CHECK("PyO3 Generator == DG1 oracle", memcmp(a, b, n) == 0);
+        CHECK("PyO3 Generator.is_complete / reset", s3dg_gen_is_complete(g) && s3dg_gen_reset(g) == 0 &&
+                                                        !s3dg_gen_is_complete(g));
+        s3dg_gen_destroy(g);
+        CHECK("PyO3 generate_data", s3dg_generate_data(a, n, 1, 1, 0, 0) == 0);
+        CHECK("PyO3 generate_data_with_threads", s3dg_generate_data(b, n, 1, 1, 0, 0) == 0 && memcmp(a, b, n) != 0);
+        free(a); free(b);
+    }
     /* generate_npz_bytes (python_datagen_api.rs:395) -> generate_npz_bytes_raw (npz.rs:322) */
     {
         s3dg_ctx *ctx = NULL;
