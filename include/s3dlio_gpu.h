@@ -207,6 +207,12 @@ int s3dg_d2h_async(s3dg_ctx *ctx, void *host, const void *dev, uint64_t len, voi
 int s3dg_h2d_async(s3dg_ctx *ctx, void *dev, const void *host, uint64_t len, void *stream);
 int s3dg_stream_create(s3dg_ctx *ctx, void **out);
 int s3dg_stream_destroy(s3dg_ctx *ctx, void *stream);
+/* Release the context's per-stream launch state (tile maps, batch staging) of
+ * `stream`, after draining it: call before destroying a stream the context has
+ * launched on, so short-lived streams do not accumulate device memory.
+ * s3dg_stream_destroy does this itself.  No-op for an unknown stream. */
+int s3dg_stream_release(s3dg_ctx *ctx, void *stream);
+int s3dg_stream_state_count(s3dg_ctx *ctx, uint64_t *n);
 int s3dg_sync(s3dg_ctx *ctx, void *stream);   /* stream NULL: whole device */
 int s3dg_device_count(int *out);
 

@@ -98,6 +98,8 @@ SIGNATURES = {
     "s3dg_host_parse_devices_env": (c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, c_int,
                                             ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_int)]),
     "s3dg_host_slot_count": (c_int, [ctypes.POINTER(c_int)]),
+    "s3dg_stream_release": (c_int, [c_vp, c_vp]),
+    "s3dg_stream_state_count": (c_int, [c_vp, ctypes.POINTER(c_u64)]),
     "s3dg_host_slot_device": (c_int, [c_int, ctypes.POINTER(c_int)]),
     "s3dg_host_slot_context": (c_int, [c_int, ctypes.POINTER(c_vp)]),
     "s3dg_generate_data": (c_int, [c_vp, c_u64, c_u64, c_u64, c_int, c_u64]),

@@ -298,33 +298,69 @@ int s3dg_ctx_create(int device, s3dg_ctx **out) {
     return S3DG_OK;
 }
 
+// Frees one stream's launch state; the caller has drained the stream (and
+// its upload stream).
+static void stream_state_free(StreamState *S) {
+    if (S->tiles) (void)hipFree(S->tiles);
+    for (int q = 0; q < 2; ++q) {
+        if (S->btiles[q]) (void)hipFree(S->btiles[q]);
+        if (S->mapped[q]) (void)hipEventDestroy(S->mapped[q]);
+        if (S->filled[q]) (void)hipEventDestroy(S->filled[q]);
+    }
+    for (auto &G : S->stage) {
+        if (G.host) (void)hipHostFree(G.host);
+        for (void *p : {(void *)G.dev, (void *)G.rec_lo, G.scan_tmp})
+            if (p) (void)hipFree(p);
+        if (G.uploaded) (void)hipEventDestroy(G.uploaded);
+        if (G.consumed) (void)hipEventDestroy(G.consumed);
+    }
+    if (S->up) (void)hipStreamDestroy(S->up);
+    delete S;
+}
+
 int s3dg_ctx_destroy(s3dg_ctx *c) {
     if (!c) return S3DG_OK;
     DeviceScope ds(c->device);
     (void)hipDeviceSynchronize();
     if (c->base_dev) (void)hipFree(c->base_dev);
-    for (auto &kv : c->streams) {
-        StreamState *S = kv.second;
-        if (S->tiles) (void)hipFree(S->tiles);
-        for (int q = 0; q < 2; ++q) {
-            if (S->btiles[q]) (void)hipFree(S->btiles[q]);
-            if (S->mapped[q]) (void)hipEventDestroy(S->mapped[q]);
-            if (S->filled[q]) (void)hipEventDestroy(S->filled[q]);
-        }
-        for (auto &G : S->stage) {
-            if (G.host) (void)hipHostFree(G.host);
-            for (void *p : {(void *)G.dev, (void *)G.rec_lo, G.scan_tmp})
-                if (p) (void)hipFree(p);
-            if (G.uploaded) (void)hipEventDestroy(G.uploaded);
-            if (G.consumed) (void)hipEventDestroy(G.consumed);
-        }
-        if (S->up) (void)hipStreamDestroy(S->up);
-        delete S;
-    }
+    for (auto &kv : c->streams) stream_state_free(kv.second);
     for (auto &kv : c->jtabs) (void)hipFree(kv.second);
     if (c->crc_tab) (void)hipFree(c->crc_tab);
     if (c->crc_seg) (void)hipFree(c->crc_seg);
     delete c;
+    return S3DG_OK;
+}
+
+// a context keeps tile maps and batch staging per stream it has
+// seen; a caller that retires a stream releases them here (after draining
+// the stream), so short-lived streams do not accumulate device memory and a
+// reused handle value starts from fresh state.
+int s3dg_stream_release(s3dg_ctx *c, void *stream) {
+    CTX_SCOPE(c);
+    StreamState *S = nullptr;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        auto it = c->streams.find((hipStream_t)stream);
+        if (it == c->streams.end()) return S3DG_OK;
+        S = it->second;
+        c->streams.erase(it);
+    }
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> g(S->mu);    // wait for an enqueue in progress; released before S is freed
+        e = hipStreamSynchronize((hipStream_t)stream);
+        if (e == hipSuccess && S->up) e = hipStreamSynchronize(S->up);
+    }
+    stream_state_free(S);
+    HIP_TRY(e, "hipStreamSynchronize(release)");
+    return S3DG_OK;
+}
+
+// Streams with launch state in this context (diagnostics and tests).
+int s3dg_stream_state_count(s3dg_ctx *c, uint64_t *n) {
+    if (!c || !n) return fail(S3DG_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    *n = c->streams.size();
     return S3DG_OK;
 }
 
@@ -1117,6 +1153,7 @@ int s3dg_stream_create(s3dg_ctx *c, void **out) {
 
 int s3dg_stream_destroy(s3dg_ctx *c, void *stream) {
     CTX_SCOPE(c);
+    if (int r = s3dg_stream_release(c, stream)) return r;
     HIP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
     return S3DG_OK;
 }

@@ -11,6 +11,7 @@
 // multiply) and hashes the sub-region tail itself.  Reads only: HBM-read bound.
 #include "s3dg_internal.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -140,6 +141,119 @@ __global__ __launch_bounds__(256) void k_crc32_regions(CrcSegArgs a, const CrcTa
     if (lane == 0) out[r] = S;
 }
 
+// ---- conflict-free form (k_crc32_regions_cf) ---------------------------------
+// The 20 lookups per 16-B piece above are ds_read_b32 with data-dependent
+// indices: 32 lanes of a half-wave pick random entries of the same 1 KiB
+// table, i.e. random banks (bank = dword address mod 32), ~3-way conflicts on
+// random data (profiles/r02/diag/crc: conflict cycles 2.04x the useful ones).
+// Here every lane of a half-wave reads a different bank at every lookup:
+//   * each table lives in ONE bank: entry i of single-bank table copy k is the
+//     dword i * 32 + k (a 256-entry table = 256 rows of one bank);
+//   * byte tables: 16 tables x 2 copies = 32 banks.  Lane l hashes its piece's
+//     bytes in a lane-dependent order: its 4 words are rotated by
+//     s = (l >> 2) & 3 (8 v_cndmask per row), and at step q it takes byte
+//     ((q + l) & 3) of rotated word q >> 2, i.e. original byte
+//     b = 4 ((q/4 + s) & 3) + ((q + l) & 3), looked up in table 15 - b, copy
+//     (l >> 4) & 1.  Over lanes 0..15 (s, l & 3) takes all 16 values, so b does:
+//     16 tables x 2 copies = 32 distinct banks per lookup;
+//   * row-advance tables: 4 tables x 8 copies.  At step k lane l looks up byte
+//     t = (k + l) & 3 of S in table t, copy (l >> 2) & 7: 32 distinct banks.
+// XOR is order-free, so the sum is the same; the bytes match k_crc32_regions
+// (and zlib) exactly.  64 KiB of LDS per workgroup: 8-wave workgroups, the
+// grid sized to the chip, each wave looping over regions.
+struct CrcTablesCF {
+    uint32_t tb[256 * 32];   // byte tables: tb[i*32 + 2t + c] = tbyte[t][i]
+    uint32_t tr[256 * 32];   // row tables:  tr[i*32 + 8t + c] = trow[t][i]
+};
+
+__global__ __launch_bounds__(512) void k_crc32_regions_cf(CrcSegArgs a, const CrcTablesCF *tabs,
+                                                          const uint32_t *lane_shift, uint32_t *out) {
+    __shared__ CrcTablesCF T;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    {
+        const uint4 *g = reinterpret_cast<const uint4 *>(tabs);
+        uint4 *d = reinterpret_cast<uint4 *>(&T);
+        for (uint32_t k = t; k < sizeof(CrcTablesCF) / 16; k += 512) d[k] = g[k];
+    }
+    __syncthreads();
+    // per-lane byte offsets (bytes) of the single-bank table copies, and the
+    // in-word byte shifts of the rotated schedule
+    const uint32_t s = (lane >> 2) & 3, cb = (lane >> 4) & 1, cr = (lane >> 2) & 7;
+    uint32_t offb[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t b = 4 * (((uint32_t)(q >> 2) + s) & 3) + (((uint32_t)q + lane) & 3);
+        offb[q] = 4 * (2 * (15 - b) + cb);
+    }
+    uint32_t shb[4], offr[4], shr[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        shb[m] = 8 * (((uint32_t)m + lane) & 3);
+        const uint32_t tt = ((uint32_t)m + lane) & 3;
+        shr[m] = 8 * tt;
+        offr[m] = 4 * (8 * tt + cr);
+    }
+    const bool rot2 = s & 2, rot1 = s & 1;
+    const uint8_t *tb = reinterpret_cast<const uint8_t *>(T.tb);
+    const uint8_t *tr = reinterpret_cast<const uint8_t *>(T.tr);
+    auto look = [&](const uint8_t *base, uint32_t byte, uint32_t off) -> uint32_t {
+        return *reinterpret_cast<const uint32_t *>(base + (byte << 7) + off);
+    };
+    auto row = [&](uint32_t S, const uint4 v) -> uint32_t {
+        // words rotated by s
+        const uint32_t x0 = rot2 ? v.z : v.x, x1 = rot2 ? v.w : v.y, x2 = rot2 ? v.x : v.z, x3 = rot2 ? v.y : v.w;
+        const uint32_t w[4] = {rot1 ? x1 : x0, rot1 ? x2 : x1, rot1 ? x3 : x2, rot1 ? x0 : x3};
+        uint32_t u[20];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            u[q] = look(tb, __builtin_amdgcn_ubfe(w[q >> 2], shb[q & 3], 8), offb[q]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) u[16 + m] = look(tr, __builtin_amdgcn_ubfe(S, shr[m], 8), offr[m]);
+        const uint32_t a0 = xor3(u[0], u[1], u[2]), a1 = xor3(u[3], u[4], u[5]), a2 = xor3(u[6], u[7], u[8]);
+        const uint32_t a3 = xor3(u[9], u[10], u[11]), a4 = xor3(u[12], u[13], u[14]);
+        const uint32_t a5 = xor3(u[15], u[16], u[17]), a6 = u[18] ^ u[19];
+        return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6);
+    };
+    const uint64_t nwaves = (uint64_t)gridDim.x * 8;
+    for (uint64_t r = (uint64_t)blockIdx.x * 8 + (t >> 6); r < a.nreg; r += nwaves) {
+        const uint64_t seg = r / a.regs_per_seg, k = r - seg * a.regs_per_seg;
+        const uint64_t row0 = k * a.rows;
+        const uint32_t nrows = (uint32_t)((a.seg_rows - row0) < a.rows ? (a.seg_rows - row0) : a.rows);
+        const uint4 *p = reinterpret_cast<const uint4 *>(a.src + seg * a.seg_stride + row0 * 1024) + lane;
+        uint32_t S = 0, rw = 0;
+        auto load4 = [&](uint4 (&v)[4], uint32_t r0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t rr = r0 + q < nrows ? r0 + q : nrows - 1;
+                v[q] = p[rr * 64];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        uint4 A[4], B[4];
+        if (nrows >= 4) load4(A, 0);
+        for (; rw + 8 <= nrows; rw += 8) {
+            load4(B, rw + 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S = row(S, A[q]);
+            __builtin_amdgcn_sched_barrier(0);
+            load4(A, rw + 8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S = row(S, B[q]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (rw + 4 <= nrows) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S = row(S, A[q]);
+            rw += 4;
+        }
+        for (; rw < nrows; ++rw) S = row(S, p[rw * 64]);
+        S = multmodp(lane_shift[lane], S);              // A^(16 (63 - lane))
+#pragma unroll
+        for (int q = 32; q >= 1; q >>= 1) S ^= __shfl_xor(S, q);
+        if (lane == 0) out[r] = S;
+    }
+}
+
 // x^(8 n) mod P (zlib x2nmodp(n, 3)) on the host.
 uint32_t x8n(uint64_t n) {
     uint32_t p = 1u << 31;           // x^0
@@ -157,6 +271,7 @@ uint32_t x8n(uint64_t n) {
 uint32_t crc_tables[8][256];
 bool tables_ready = false;
 CrcTables dev_tables_host;
+CrcTablesCF dev_tables_cf_host;
 uint32_t lane_shift_host[64];
 
 void init_tables() {
@@ -181,6 +296,12 @@ void init_tables() {
     for (int b = 0; b < 4; ++b)
         for (uint32_t x = 0; x < 256; ++x) dev_tables_host.trow[b][x] = multmodp(x1k, x << (8 * b));
     for (int l = 0; l < 64; ++l) lane_shift_host[l] = x8n(16ull * (63 - l));
+    for (uint32_t i = 0; i < 256; ++i) {
+        for (int t = 0; t < 16; ++t)
+            for (int c = 0; c < 2; ++c) dev_tables_cf_host.tb[i * 32 + 2 * t + c] = dev_tables_host.tbyte[t][i];
+        for (int t = 0; t < 4; ++t)
+            for (int c = 0; c < 8; ++c) dev_tables_cf_host.tr[i * 32 + 8 * t + c] = dev_tables_host.trow[t][i];
+    }
     tables_ready = true;
 }
 
@@ -219,11 +340,24 @@ hipError_t crc_tables_device(void **tab_cache) {
     }
     if (*tab_cache) return hipSuccess;
     hipError_t e;
-    if ((e = hipMalloc(tab_cache, sizeof(CrcTables) + 64 * 4)) != hipSuccess) return e;
+    // [CrcTables][lane shifts, 256 B][CrcTablesCF]
+    if ((e = hipMalloc(tab_cache, sizeof(CrcTables) + 64 * 4 + sizeof(CrcTablesCF))) != hipSuccess) return e;
     if ((e = hipMemcpy(*tab_cache, &dev_tables_host, sizeof(CrcTables), hipMemcpyHostToDevice)) != hipSuccess)
         return e;
-    return hipMemcpy((uint8_t *)*tab_cache + sizeof(CrcTables), lane_shift_host, 64 * 4,
+    if ((e = hipMemcpy((uint8_t *)*tab_cache + sizeof(CrcTables), lane_shift_host, 64 * 4,
+                       hipMemcpyHostToDevice)) != hipSuccess)
+        return e;
+    return hipMemcpy((uint8_t *)*tab_cache + sizeof(CrcTables) + 64 * 4, &dev_tables_cf_host, sizeof(CrcTablesCF),
                      hipMemcpyHostToDevice);
+}
+
+// 0: k_crc32_regions_cf (default), 1: k_crc32_regions (env S3DG_CRC_KERNEL=1; A/B only, same bytes)
+int crc_kernel_choice() {
+    static const int k = [] {
+        const char *v = getenv("S3DG_CRC_KERNEL");
+        return v && v[0] == '1' ? 1 : 0;
+    }();
+    return k;
 }
 
 CrcSegPlan crc_seg_plan(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride) {
@@ -244,10 +378,20 @@ hipError_t crc_seg_launch(const CrcSegPlan &P, const uint8_t *dev, void *tab_dev
                           hipStream_t s) {
     if (P.nreg == 0) return hipSuccess;
     CrcSegArgs a{dev, P.nreg, P.regs_per_seg, P.seg_stride, P.seg_rows, P.rows};
-    const uint64_t wgs = (P.nreg + 3) / 4;
+    const uint32_t *lsh = (const uint32_t *)((uint8_t *)tab_dev + sizeof(CrcTables));
     (void)hipGetLastError();
-    hipLaunchKernelGGL(k_crc32_regions, dim3((uint32_t)wgs), dim3(256), 0, s, a, (const CrcTables *)tab_dev,
-                       (const uint32_t *)((uint8_t *)tab_dev + sizeof(CrcTables)), out_dev);
+    if (crc_kernel_choice() == 0) {
+        // conflict-free form: 8-wave workgroups, 2 per CU (64 KiB LDS each),
+        // every wave looping over regions
+        const uint64_t need = (P.nreg + 7) / 8;
+        const uint32_t wgs = (uint32_t)(need < 512 ? need : 512);
+        hipLaunchKernelGGL(k_crc32_regions_cf, dim3(wgs), dim3(512), 0, s, a,
+                           (const CrcTablesCF *)((uint8_t *)tab_dev + sizeof(CrcTables) + 64 * 4), lsh, out_dev);
+    } else {
+        const uint64_t wgs = (P.nreg + 3) / 4;
+        hipLaunchKernelGGL(k_crc32_regions, dim3((uint32_t)wgs), dim3(256), 0, s, a, (const CrcTables *)tab_dev, lsh,
+                           out_dev);
+    }
     return hipGetLastError();
 }
 

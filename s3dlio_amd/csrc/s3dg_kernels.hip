@@ -446,33 +446,59 @@ __device__ PrefixParams dev_make_prefix(uint64_t nb, uint64_t dedup, uint32_t f_
 // = the object's granule mod 8 (XCD alignment).  Dense: rec_lo = the object's
 // granule slot (0 for the first object, whose lead is lead0), rec_hi = the
 // next object's, so the gap records before it are its dead slots.
+// An object with few records writes them itself; the records of objects with
+// more (a multi-GiB object, a dense layout with large gaps) are written by the
+// whole wave, 64 per pass, so no lane loops over tens of thousands of them
+// while the fill waits.
+constexpr uint64_t kMapOwnRecords = 16;
 __global__ __launch_bounds__(256) void k_batch_map(const s3dg_obj_desc *d, uint64_t n, const uint64_t *scan,
                                                    TileRec *tiles, uint32_t tshift, uint64_t base, uint64_t lead0,
                                                    uint64_t first_off) {
     const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k >= n) return;
-    const s3dg_obj_desc o = d[k];
-    const uint64_t nb = (o.size + kBlk - 1) / kBlk;
-    uint64_t rec_lo, rec_hi, lead;
-    if (tshift == 0) {
-        const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
-        rec_lo = k == 0 ? 0 : g0;
-        rec_hi = k + 1 < n ? lead0 + (d[k + 1].dst_off - first_off) / kBlk : g0 + nb;
-        lead = g0 - rec_lo;
-    } else {
-        lead = ((base + o.dst_off) >> 12) & 7;
-        rec_lo = scan[k];
-        rec_hi = rec_lo + ((nb + lead + (1ull << tshift) - 1) >> tshift);
+    const uint32_t lane = threadIdx.x & 63;
+    TileRec r{};
+    uint64_t rec_lo = 0, rec_hi = 0;
+    if (k < n) {
+        const s3dg_obj_desc o = d[k];
+        const uint64_t nb = (o.size + kBlk - 1) / kBlk;
+        uint64_t lead;
+        if (tshift == 0) {
+            const uint64_t g0 = lead0 + (o.dst_off - first_off) / kBlk;
+            rec_lo = k == 0 ? 0 : g0;
+            rec_hi = k + 1 < n ? lead0 + (d[k + 1].dst_off - first_off) / kBlk : g0 + nb;
+            lead = g0 - rec_lo;
+        } else {
+            lead = ((base + o.dst_off) >> 12) & 7;
+            rec_lo = scan[k];
+            rec_hi = rec_lo + ((nb + lead + (1ull << tshift) - 1) >> tshift);
+        }
+        r.dst_off = o.dst_off;
+        r.size = o.size;
+        r.entropy = o.entropy;
+        r.lead = (uint32_t)lead;
+        r.pp = dev_make_prefix(nb, o.dedup, o.f_num, o.f_den);
     }
-    TileRec r;
-    r.dst_off = o.dst_off;
-    r.size = o.size;
-    r.entropy = o.entropy;
-    r.lead = (uint32_t)lead;
-    r.pp = dev_make_prefix(nb, o.dedup, o.f_num, o.f_den);
-    for (uint64_t q = rec_lo; q < rec_hi; ++q) {
-        r.first = (uint32_t)((q - rec_lo) << tshift);
-        tiles[q] = r;
+    const bool own = rec_hi - rec_lo <= kMapOwnRecords;
+    if (own)
+        for (uint64_t q = rec_lo; q < rec_hi; ++q) {
+            r.first = (uint32_t)((q - rec_lo) << tshift);
+            tiles[q] = r;
+        }
+    // the wave's objects with many records, one after the other, 64 records per pass
+    uint64_t big = __ballot(!own);
+    while (big) {
+        const int src = __builtin_ctzll(big);
+        big &= big - 1;
+        TileRec b;
+        uint32_t *bw = reinterpret_cast<uint32_t *>(&b);
+        const uint32_t *rw = reinterpret_cast<const uint32_t *>(&r);
+#pragma unroll
+        for (int w = 0; w < 16; ++w) bw[w] = __builtin_amdgcn_readlane(rw[w], src);
+        const uint64_t lo = readlane64(rec_lo, src), hi = readlane64(rec_hi, src);
+        for (uint64_t q = lo + lane; q < hi; q += 64) {
+            b.first = (uint32_t)((q - lo) << tshift);
+            tiles[q] = b;
+        }
     }
 }
 

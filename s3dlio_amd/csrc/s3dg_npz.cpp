@@ -146,6 +146,9 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
             uint64_t cap = 0;
             hipStream_t s = nullptr, s_crc = nullptr;   // D2H stream, CRC stream
             hipEvent_t filled = nullptr;
+            void *crc_tab = nullptr;                     // CRC tables (device)
+            uint32_t *reg = nullptr;                     // region CRCs (device)
+            uint64_t reg_cap = 0;
         };
         static std::mutex map_mu;
         static std::map<int, Cache *> *caches = new std::map<int, Cache *>();   // never freed: outlives HIP
@@ -184,12 +187,31 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
         // keystream: the CRC runs on a second stream, hidden under the copy.
         if (hipEventRecord(C->filled, s) != hipSuccess || hipStreamWaitEvent(C->s_crc, C->filled, 0) != hipSuccess)
             return s3dg_internal_fail(S3DG_EHIP, "npz event");
-        if (hipMemcpyAsync(out + L.off_x_data, dev, L.x_data, hipMemcpyDeviceToHost, s) != hipSuccess)
+        // The CRC kernel is enqueued first on its own stream, then the D2H
+        // (which, into pageable memory, returns only when done): the two
+        // overlap on the GPU.  The region CRCs are fetched after the D2H, and
+        // the < 1 KiB tail is hashed from the host copy, so no two copies are
+        // in flight from two host threads.
+        if (crc_tables_device(&C->crc_tab) != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, "crc tables");
+        const CrcSegPlan P = crc_seg_plan(1, L.x_data, L.x_data);
+        if (P.nreg > C->reg_cap) {
+            if (C->reg) (void)hipFree(C->reg);
+            C->reg = nullptr;
+            C->reg_cap = 0;
+            if (hipMalloc(&C->reg, P.nreg * 4) != hipSuccess) return s3dg_internal_fail(S3DG_ENOMEM, "hipMalloc(crc)");
+            C->reg_cap = P.nreg;
+        }
+        if (crc_seg_launch(P, (const uint8_t *)dev, C->crc_tab, C->reg, C->s_crc) != hipSuccess)
+            return s3dg_internal_fail(S3DG_EHIP, "launch k_crc32_regions");
+        if (hipMemcpyAsync(out + L.off_x_data, dev, L.x_data, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
             return s3dg_internal_fail(S3DG_EHIP, "npz x-data D2H");
-        const int rc = s3dg_internal_crc_device(ctx, dev, L.x_data, C->s_crc, &cd);   // waits for s_crc only
-        const hipError_t es = hipStreamSynchronize(s);
-        if (rc) return rc;
-        if (es != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, "npz sync");
+        std::vector<uint32_t> regions(P.nreg);
+        if (P.nreg && (hipMemcpyAsync(regions.data(), C->reg, P.nreg * 4, hipMemcpyDeviceToHost, C->s_crc) != hipSuccess ||
+                       hipStreamSynchronize(C->s_crc) != hipSuccess))
+            return s3dg_internal_fail(S3DG_EHIP, "npz crc regions");
+        const uint8_t *tail = out + L.off_x_data + P.seg_rows * 1024;
+        crc_seg_fold(P, regions.data(), &tail, &cd);
         crc_x = crc32_combine(crc_x, cd, L.x_data);                                    // :386
     }
     // x.npy: local header + NPY header (:368-372, patched :389-392)

@@ -318,6 +318,17 @@ class Context:
     def sync(self, stream=None) -> None:
         call("s3dg_sync", self._h, 0 if stream is None else _stream(stream))
 
+    def release_stream(self, stream) -> None:
+        """Drain `stream` and free this context's launch state for it (tile
+        maps, batch staging; s3dg_stream_release).  Call before a stream the
+        context launched on goes away."""
+        call("s3dg_stream_release", self._h, _stream(stream))
+
+    def stream_state_count(self) -> int:
+        n = ctypes.c_uint64()
+        call("s3dg_stream_state_count", self._h, ctypes.byref(n))
+        return n.value
+
 
 def xoshiro_jump(state, n: int) -> list[int]:
     """Host jump-ahead of a Xoshiro256 state by n steps (the kernels' method)."""

@@ -85,3 +85,39 @@ def test_no_device_or_host_leak_across_repeated_calls(tmp_path):
     r1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
     assert d1 - d0 < 64 << 20, (d0, d1)        # device memory flat (allocator noise only)
     assert (r1 - r0) * 1024 < 512 << 20, (r0, r1)
+
+
+@pytest.mark.gpu
+def test_stream_release_frees_per_stream_state(oracle):
+    """tiled launches on many short-lived streams keep one launch
+    state each until s3dg_stream_release; after release the count drops, device
+    memory returns, and a reused stream starts fresh with exact bytes."""
+    import torch
+    import s3dlio_amd as S
+    MiB = 1 << 20
+    ctx = S.Context(0, base_seed=S.DEFAULT_BASE_SEED)
+    buf = torch.empty(80 * MiB, dtype=torch.uint8, device="cuda")
+    exp = oracle.fill_controlled(80 * MiB, 1, 0, 1, 5, oracle.base_block(S.DEFAULT_BASE_SEED))
+
+    def dev_used():
+        torch.cuda.synchronize()
+        free, total = torch.cuda.mem_get_info()
+        return total - free
+
+    before = ctx.stream_state_count()
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    for s in streams:                       # >= 64 MiB: the tiled path, one tile map per stream
+        ctx.fill_controlled(buf, 80 * MiB, dedup=1, compress=1, entropy=5, stream=s)
+        ctx.fill_batch(buf, [(0, 3 * MiB, 1, 1, 1)], stream=s)
+    torch.cuda.synchronize()
+    assert ctx.stream_state_count() >= before + 6
+    used = dev_used()
+    for s in streams:
+        ctx.release_stream(s)
+    assert ctx.stream_state_count() == before
+    assert dev_used() <= used
+    ctx.release_stream(streams[0])          # unknown now: no-op
+    ctx.fill_controlled(buf, 80 * MiB, dedup=1, compress=1, entropy=5, stream=streams[0])
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), exp)
+    del ctx
