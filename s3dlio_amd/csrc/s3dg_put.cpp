@@ -356,7 +356,14 @@ int run_lane(const PutArgs &A, s3dg_ctx *ctx, PutPool &P, int lane, uint64_t j0,
     std::shared_ptr<OpenFile> cur_file;   // split object being written
     uint32_t cur_crc = 0;
 
-    auto enqueue = [&](uint64_t ci) -> int {
+    // Per chunk, in stream order on its device slot's stream: the fill, the
+    // CRC kernel, the region CRCs to the host, then (enqueue_d2h) the payload
+    // D2H and the completion event.  The next chunk's fill and CRC are
+    // enqueued on the other stream BEFORE this chunk's payload D2H, so they
+    // run under the copy even when the runtime returns from the D2H call only
+    // once the copy is done (it does for blit copies; rocprof trace,
+    // DESIGN.md §5.4).
+    auto enqueue_gen = [&](uint64_t ci) -> int {
         const ChunkDesc &c = chunks[ci];
         const int ds = (int)(ci & 1), hs = (int)(ci % kHostSlots);
         hipStream_t s = P.st[ds];
@@ -377,12 +384,20 @@ int run_lane(const PutArgs &A, s3dg_ctx *ctx, PutPool &P, int lane, uint64_t j0,
         const CrcSegPlan cp = crc_seg_plan(c.n_objs, c.len, stride);
         if (cp.nreg > kMaxRegions) return s3dg_internal_fail(S3DG_EINVAL, "crc region table overflow");
         PUT_HIP(crc_seg_launch(cp, d, P.crc_tab, P.dev_reg[ds], s), "launch k_crc32_regions");
-        W.wait_slot(lane, hs);                             // writers done with chunk ci - kHostSlots
+        // host_reg[hs] was last read by complete(ci - kHostSlots), already done
         if (cp.nreg)
             PUT_HIP(hipMemcpyAsync(P.host_reg[hs], P.dev_reg[ds], cp.nreg * 4, hipMemcpyDeviceToHost, s),
                     "hipMemcpyAsync(crc regions)");
+        return S3DG_OK;
+    };
+    auto enqueue_d2h = [&](uint64_t ci) -> int {
+        const ChunkDesc &c = chunks[ci];
+        const int ds = (int)(ci & 1), hs = (int)(ci % kHostSlots);
+        hipStream_t s = P.st[ds];
+        W.wait_slot(lane, hs);                             // writers done with chunk ci - kHostSlots
         const uint64_t bytes = (c.n_objs - 1) * stride + c.len;
-        PUT_HIP(hipMemcpyAsync(P.host[hs], d, bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync(D2H payload)");
+        PUT_HIP(hipMemcpyAsync(P.host[hs], P.dev[ds], bytes, hipMemcpyDeviceToHost, s),
+                "hipMemcpyAsync(D2H payload)");
         PUT_HIP(hipEventRecord(P.ev[hs], s), "hipEventRecord");
         return S3DG_OK;
     };
@@ -443,8 +458,13 @@ int run_lane(const PutArgs &A, s3dg_ctx *ctx, PutPool &P, int lane, uint64_t j0,
     };
 
     int rc = S3DG_OK;
+    if (!chunks.empty()) rc = enqueue_gen(0);
     for (uint64_t ci = 0; ci < chunks.size() && rc == S3DG_OK && !W.failed.load(); ++ci) {
-        if ((rc = enqueue(ci)) != S3DG_OK) break;
+        // chunk ci+1's fill + CRC (other stream) go in before chunk ci's payload
+        // D2H; its device chunk was last copied out by chunk ci-1's D2H, earlier
+        // on the same stream
+        if (ci + 1 < chunks.size() && (rc = enqueue_gen(ci + 1)) != S3DG_OK) break;
+        if ((rc = enqueue_d2h(ci)) != S3DG_OK) break;
         if (ci > 0) rc = complete(ci - 1);
     }
     if (rc == S3DG_OK && !W.failed.load() && !chunks.empty()) rc = complete(chunks.size() - 1);

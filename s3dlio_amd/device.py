@@ -258,7 +258,13 @@ class Context:
              self._s(stream))
 
     def fill_batch(self, dst, objects, stream=None) -> None:
-        """objects: iterable of (dst_off, size, entropy, dedup, compress)."""
+        """objects: iterable of (dst_off, size, entropy, dedup, compress).
+
+        The descriptors are checked here first (bounds against `dst`), and the
+        library validates them again sub-batch by sub-batch (16 Ki objects,
+        doubling) while earlier sub-batches are already enqueued: a call that
+        raises on an invalid descriptor past the first sub-batch may have
+        written the objects before it (include/s3dlio_gpu.h)."""
         objs = list(objects)
         arr = (ObjDesc * max(1, len(objs)))()
         need = 0
