@@ -18,12 +18,17 @@ the batch API, 8/9 config 1's 64 KiB objects on the GPU (stream / batch API),
 s3dg_fill_controlled call on a single 1/4/16 MiB buffer (the reference's own
 criterion shape, benches/performance_microbenchmarks.rs:43-64), 14/15 the
 DG1 byte path behind generate_data / Generator (one launch per object), 16/17
-the same objects through s3dg_dgen_fill_stream (one launch per step).
+the same objects through s3dg_dgen_fill_stream (one launch per step), 18-22
+the host-buffer drop-ins (the reference's own API: s3dlio_fill_controlled_data
+on 1/4/16 MiB and 1 GiB host buffers from a native loop, generate_into_buffer
+from 8 threads; --host-mem pageable|pinned; roofline bound = PCIe).
+--d2h-full: the D2H-inclusive rate over the rank's whole object range (config 5
+as BASELINE states it), not an 8 GiB sample.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
-`roofline` (kernel-event timing vs the 8 TB/s HBM peak, and vs the fill's own
-store-only ceiling) and `cpu_baseline` (the C port of the same generator on
-this host's cores — rank 0 at N=1 only).
+`roofline` (kernel-event timing vs the 8 TB/s HBM peak; the fill's store-only
+reference shapes beside it, which the fill beats) and `cpu_baseline` (the C
+port of the same generator on this host's cores — rank 0 at N=1 only).
 """
 from __future__ import annotations
 

@@ -367,7 +367,19 @@ CrcSegPlan crc_seg_plan(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride) {
     P.seg_stride = seg_stride;
     P.seg_rows = seg_len / 1024;
     uint32_t rows = 256;                                   // 256 KiB per wave region
+    // smaller regions when 256 KiB ones would not give about one wave per
+    // resident slot (4096): a 256 MiB PUT chunk or a 140 MiB NPZ archive
+    // otherwise runs 1024 / 560 waves on 256 CUs (32 KiB minimum)
+    const uint64_t total_rows = nseg * P.seg_rows;
+    if (total_rows / rows < 4096) {
+        const uint64_t r = total_rows / 4096;
+        rows = (uint32_t)(r < 32 ? 32 : r);
+    }
     while (nseg * ((P.seg_rows + rows - 1) / rows) > (1ull << 24)) rows *= 2;
+    // one large segment: at most 4096 regions (about one per resident wave),
+    // so the host folds a few thousand region CRCs, not one per 256 KiB
+    // (16 GiB: 65 536 -> 4096)
+    while (nseg == 1 && (P.seg_rows + rows - 1) / rows > 4096) rows *= 2;
     P.rows = rows;
     P.regs_per_seg = (P.seg_rows + rows - 1) / rows;
     P.nreg = nseg * P.regs_per_seg;

@@ -12,11 +12,12 @@
 //
 // Pipeline (one call):
 //   generator thread: chunk c -> device slot c&1 on stream c&1:
-//       fill kernel(s) -> k_crc32_regions over the chunk's objects ->
-//       D2H region CRCs + payload into pinned host slot c%kHostSlots -> event
-//     then finishes chunk c-1 (event wait, CRC fold, framing) and queues its
-//     objects to the writers; a host slot is reused only after every write
-//     from it has completed.
+//       fill kernel(s) -> k_crc32_regions over the chunk's objects (region
+//       CRCs written straight into pinned host slot c%kHostSlots); chunk
+//       c+1's fill + CRC are enqueued on the other stream, then chunk c's
+//       payload D2H into the host slot -> event; then it finishes chunk c-1
+//     (event wait, CRC fold, framing) and queues its objects to the writers;
+//     a host slot is reused only after every write from it has completed.
 //   writer threads (max_in_flight): open/create, pwritev(prefix, payload,
 //     suffix) straight from pinned memory, close.
 // Objects larger than a slot are split into slot-sized pieces that share
@@ -68,7 +69,8 @@ using namespace s3dg;
 
 constexpr uint64_t kSlotBytes = 256ull << 20;   // device chunk / host slot (multiple of 1 MiB)
 constexpr int kHostSlots = 4;
-constexpr uint64_t kMaxRegions = kSlotBytes / kBlk + kSlotBytes / (256 * 1024) + 16;
+// one region per object plus at most 4096 more (crc_seg_plan sizes regions for ~4096)
+constexpr uint64_t kMaxRegions = kSlotBytes / kBlk + 4096 + kSlotBytes / (256 * 1024) + 16;
 
 // Process-wide buffers per (device, lane), created on first use and reused;
 // a lane's pool is held (mutex) for the duration of a call.
@@ -77,7 +79,6 @@ struct PutPool {
     bool ready = false;
     int device = -1;
     void *dev[2] = {nullptr, nullptr};
-    uint32_t *dev_reg[2] = {nullptr, nullptr};
     hipStream_t st[2] = {nullptr, nullptr};
     uint8_t *host[kHostSlots] = {};
     uint32_t *host_reg[kHostSlots] = {};
@@ -108,12 +109,12 @@ int pool_init(PutPool &P, int device) {
     PUT_HIP(hipSetDevice(device), "hipSetDevice");
     for (int k = 0; k < 2; ++k) {
         PUT_HIP(hipMalloc(&P.dev[k], kSlotBytes), "hipMalloc(put chunk)");
-        PUT_HIP(hipMalloc(&P.dev_reg[k], kMaxRegions * 4), "hipMalloc(put crc regions)");
         PUT_HIP(hipStreamCreateWithFlags(&P.st[k], hipStreamNonBlocking), "hipStreamCreate");
     }
     NumaScope numa(device);            // the pinned ring on the GPU's NUMA node
     for (int k = 0; k < kHostSlots; ++k) {
         PUT_HIP(hipHostMalloc((void **)&P.host[k], kSlotBytes, hipHostMallocDefault), "hipHostMalloc(put ring)");
+        // written by the CRC kernel directly (pinned host memory is device-visible)
         PUT_HIP(hipHostMalloc((void **)&P.host_reg[k], kMaxRegions * 4, hipHostMallocDefault),
                 "hipHostMalloc(put crc regions)");
         PUT_HIP(hipEventCreateWithFlags(&P.ev[k], hipEventDisableTiming), "hipEventCreate");
@@ -383,11 +384,12 @@ int run_lane(const PutArgs &A, s3dg_ctx *ctx, PutPool &P, int lane, uint64_t j0,
         }
         const CrcSegPlan cp = crc_seg_plan(c.n_objs, c.len, stride);
         if (cp.nreg > kMaxRegions) return s3dg_internal_fail(S3DG_EINVAL, "crc region table overflow");
-        PUT_HIP(crc_seg_launch(cp, d, P.crc_tab, P.dev_reg[ds], s), "launch k_crc32_regions");
-        // host_reg[hs] was last read by complete(ci - kHostSlots), already done
-        if (cp.nreg)
-            PUT_HIP(hipMemcpyAsync(P.host_reg[hs], P.dev_reg[ds], cp.nreg * 4, hipMemcpyDeviceToHost, s),
-                    "hipMemcpyAsync(crc regions)");
+        // The kernel writes the region CRCs straight into the pinned host slot
+        // (a few KiB over PCIe): no D2H call here, because the runtime returns
+        // from a D2H call only when the copy is done (rocprof trace, DESIGN.md
+        // §5.4), which would hold this thread until the fill and CRC finish.
+        // host_reg[hs] was last read by complete(ci - kHostSlots), already done.
+        PUT_HIP(crc_seg_launch(cp, d, P.crc_tab, P.host_reg[hs], s), "launch k_crc32_regions");
         return S3DG_OK;
     };
     auto enqueue_d2h = [&](uint64_t ci) -> int {

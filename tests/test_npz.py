@@ -60,3 +60,31 @@ def test_gpu_crc32_vs_zlib(gpu_ctx, n):
     host = torch.randint(0, 256, (max(n, 1),), dtype=torch.uint8, generator=g)[:n]
     dev = host.cuda() if n else torch.empty(16, dtype=torch.uint8, device="cuda")
     assert S.crc32_device(gpu_ctx, dev, n) == zlib.crc32(host.numpy().tobytes())
+
+
+@pytest.mark.gpu
+def test_gpu_crc32_large_single_segment(gpu_ctx):
+    """> 1 GiB in one segment: the plan widens regions past 256 KiB (at most
+    4096 regions) and both CRC kernels agree with zlib."""
+    import subprocess
+    import sys
+    import torch
+    import s3dlio_amd as S
+    n = 1536 * 2**20 + 5
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu_ctx.xoshiro_fill(dev, n, 2 << 20, seed_base=3)
+    torch.cuda.synchronize()
+    host = dev.cpu().numpy()
+    exp = zlib.crc32(memoryview(host))
+    assert S.crc32_device(gpu_ctx, dev, n) == exp
+    del dev, host
+    # the round-2 kernel (S3DG_CRC_KERNEL=1, read once per process) in a child
+    code = ("import sys, zlib, torch; sys.path.insert(0, sys.argv[1]); import s3dlio_amd as S; "
+            "c = S.Context(0); n = 1536 * 2**20 + 5; d = torch.empty(n, dtype=torch.uint8, device='cuda'); "
+            "c.xoshiro_fill(d, n, 2 << 20, seed_base=3); torch.cuda.synchronize(); "
+            f"assert S.crc32_device(c, d, n) == {exp}; print('ok')")
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code, root], env=dict(os.environ, S3DG_CRC_KERNEL="1"),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
