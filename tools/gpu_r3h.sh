@@ -14,3 +14,5 @@ PUT_N=1024 timeout -k 10 300 python -u tools/bench_put.py > $OUT/put_bench.log 2
 grep '^{' $OUT/put_bench.log
 timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/crc_tl -o t --output-format csv -- python3 tools/crc_timeline.py run > $OUT/crc_tl.log 2>&1 || { tail $OUT/crc_tl.log; exit 1; }
 python3 tools/crc_timeline.py summarize $OUT/crc_tl | tee $OUT/crc_tl_summary.json
+timeout -k 10 200 python -u tools/hostbuf_lab.py > $OUT/hostbuf_lab.log 2>&1 || { tail $OUT/hostbuf_lab.log; exit 1; }
+grep '^{' $OUT/hostbuf_lab.log
