@@ -22,6 +22,8 @@
 //     are recomputed, never copied.
 #include "s3dg_internal.h"
 
+#include <cstdlib>
+
 // Diagnostic builds only (tools/ablate.py): bit 0 = no window patch phase,
 // bit 1 = no PRNG chain; k_keystream: bit 5 = no Xoshiro steps in the draw
 // loop (counter draws), bit 6 = no jump-ahead.  Outputs of such builds are
@@ -868,6 +870,24 @@ constexpr uint32_t ks_static_lds(int D, int W) { return (uint32_t)W * 64u * (uin
 // Grid sizes are 32-bit WORK-ITEM counts in the AQL dispatch packet: cap a
 // launch at 2^22 workgroups per dimension (x 256 threads < 2^32).
 constexpr uint64_t kMaxGridX = 1ull << 22;
+// Batch launches (k_fill_batch, 64 x NW threads): the largest multiple of 256
+// workgroups (XCD dealing and the prefetch spans restart at each launch) whose
+// work items still fit in 32 bits, so a config-2 step (20.5 M blocks) is one
+// launch instead of five.  Env S3DG_BATCH_GRID_CAP (a multiple of 256)
+// overrides it, for A/Bs and for the tests of the split path.
+uint64_t batch_grid_cap(int nw) {
+#ifdef S3DG_DIAG_GRID_CAP
+    (void)nw;
+    return S3DG_DIAG_GRID_CAP;   // diagnostic builds (tools/variant_lab.py A/B)
+#endif
+    static const uint64_t env = [] {
+        const char *v = getenv("S3DG_BATCH_GRID_CAP");
+        const uint64_t x = v ? strtoull(v, nullptr, 10) : 0;
+        return x >= 256 ? x & ~255ull : 0ull;
+    }();
+    const uint64_t lim = (0xFFFFFFFFull / (64ull * (uint64_t)nw)) & ~255ull;
+    return env && env < lim ? env : lim;
+}
 
 template <int NT, int NW>
 void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const u32x4 *b, uint64_t stride,
@@ -973,8 +993,9 @@ static hipError_t batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t t
     hipError_t e;
     const u32x4 *b = reinterpret_cast<const u32x4 *>(base_dev);
     const uint64_t total = total_tiles << tshift;
-    for (uint64_t g0 = 0; g0 < total; g0 += kMaxGridX) {
-        const uint32_t gx = (uint32_t)((total - g0) < kMaxGridX ? (total - g0) : kMaxGridX);
+    const uint64_t cap = batch_grid_cap(lc.waves_per_block);
+    for (uint64_t g0 = 0; g0 < total; g0 += cap) {
+        const uint32_t gx = (uint32_t)((total - g0) < cap ? (total - g0) : cap);
         if (ablated)
             S3DG_DISPATCH(launch_batch_abl_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
                           lc.prefetch_tiles, tshift, b, lc.pace);

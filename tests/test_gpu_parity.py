@@ -510,9 +510,10 @@ def test_keystream_full_size_properties(gpu_ctx, torch, oracle):
 
 
 def test_launch_splitting_large_grids(gpu_ctx, torch, oracle, base):
-    """Launches are split at 2^22 workgroups per grid dimension (AQL grid
-    sizes are 32-bit work-item counts).  One 17 GiB object (stream path) and a
-    17.5 GiB batch both cross that split; both checked against the oracle."""
+    """Large grids: a 17 GiB object and 17.5 GiB batches with 1, 2 and 4 waves
+    per block (AQL grid sizes are 32-bit work-item counts; batch launches are
+    capped at the largest multiple of 256 workgroups that fits, the 2D stream
+    kernel at 2^22 per dimension); checked against the oracle."""
     size = 17 * 2**30 + 4096 * 3 + 5
     t = torch.empty(size, dtype=torch.uint8, device="cuda")
     gpu_ctx.fill_controlled(t, size, dedup=1, compress=3, entropy=123)
@@ -554,3 +555,49 @@ def test_block_windows_equal_rand_crate_vectors(gpu_ctx, torch):
     torch.cuda.synchronize()
     h = bytes(u[4096:].cpu().numpy())
     assert h[:32] == want1 and h[2048:2080] == want2
+
+
+def test_batch_launch_split_path(tmp_path):
+    """The split path of batch launches, forced in a child process with a small
+    cap (S3DG_BATCH_GRID_CAP=2^20 workgroups): a 5 GiB tiled fill and a batch
+    of 3 x 1.5 GiB objects cross several launch boundaries; every byte of the
+    boundary windows and the last object equals the oracle."""
+    import subprocess
+    import sys
+    script = r'''
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch
+import s3dlio_amd as S
+from oracle import oracle_c as OC
+from oracle import oracle_py as P
+base = OC.base_block(S.DEFAULT_BASE_SEED)
+ctx = S.Context(0, base_seed=S.DEFAULT_BASE_SEED)
+size = 5 * 2**30 + 4096 + 7
+t = torch.empty(size, dtype=torch.uint8, device="cuda")
+ctx.fill_controlled(t, size, dedup=3, compress=2, entropy=55)
+torch.cuda.synchronize()
+exp = OC.fill_controlled(size, 3, 1, 2, 55, base)
+for k in range(1, 6):                      # every 2^20-block (4 GiB) launch boundary +- 1 MiB
+    lo = max(0, k * 2**32 - 2**20); hi = min(size, k * 2**32 + 2**20)
+    if lo < size:
+        assert np.array_equal(t[lo:hi].cpu().numpy(), exp[lo:hi]), k
+assert np.array_equal(t[size - 2**20:].cpu().numpy(), exp[size - 2**20:])
+del t, exp
+osz = 3 * 2**29 + 9
+stride = (osz + 4095) // 4096 * 4096
+objs = [(k * stride, osz, P.object_entropy(0x5EED000000000001, k), 1, 1) for k in range(3)]
+out = torch.empty(3 * stride, dtype=torch.uint8, device="cuda")
+ctx.fill_batch(out, objs)
+torch.cuda.synchronize()
+exp = OC.fill_controlled(osz, 1, 0, 1, P.object_entropy(0x5EED000000000001, 2), base)
+assert np.array_equal(out[2 * stride:2 * stride + osz].cpu().numpy(), exp)
+print("split ok")
+'''
+    p = tmp_path / "split.py"
+    p.write_text(script)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, S3DG_BATCH_GRID_CAP=str(1 << 20))
+    r = subprocess.run([sys.executable, str(p), root], env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0 and "split ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
