@@ -63,6 +63,7 @@ def main():
         libs[name] = (L, h)
     descs = {}
     for kind, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3), ("cfg7", [8 * MiB] * n, 1, 0, 1),
+                                   ("cfg4d1", log_uniform_sizes(n), 1, 0, 1), ("cfg4c1", log_uniform_sizes(n), 2, 0, 1),
                                    ("small", log_uniform_sizes(10 * n, 5, 4096, MiB), 1, 0, 1),
                                    ("mid", [MiB + 123] * (5 * n), 3, 2, 3),
                                    ("kb64", [64 << 10] * (10 * n), 1, 0, 1),
