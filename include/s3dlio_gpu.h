@@ -78,7 +78,11 @@ int s3dg_set_nontemporal(s3dg_ctx *ctx, int on);
 int s3dg_set_store_policy(s3dg_ctx *ctx, int stream_policy, int batch_policy);
 /* Cap on resident fill workgroups per CU (reserved LDS), for stream and
  * batch launches separately; 0 = hardware maximum, negative = the default.
- * Defaults 14 (stream) and 0 (batch), measured on MI355X.  A tuning knob; results are identical. */
+ * Defaults, measured on MI355X: 14 (stream); batch launches (and large
+ * uniform streams, which run through the batch kernel) per launch: no cap,
+ * or 30 when most of the launch's blocks have a zero prefix ending on a 64-B
+ * line (64 f_num / f_den whole: compress 2, 4, 8, ...).  A tuning knob; results
+ * are identical. */
 int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_cu);
 /* Batch launches: distance (in units of 64 blocks) at which workgroups warm
  * the L2 with later tile records; 0 = off, UINT32_MAX = default (256).
@@ -112,7 +116,9 @@ int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int 
  * identical. */
 int s3dg_set_keystream_xcd_group(s3dg_ctx *ctx, int mode, uint32_t waves);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
-/* Resident workgroups per CU the current settings give (HIP occupancy API). */
+/* Resident workgroups per CU the current settings give (HIP occupancy API):
+ * batch 0 = stream launches, 1 = batch launches, 2 = batch launches whose
+ * zero prefixes end on a 64-B line (see s3dg_set_occupancy). */
 int s3dg_query_occupancy(s3dg_ctx *ctx, int batch, int *wgs_per_cu);
 
 /* ---- parameter helpers (host math shared with the kernels) --------------- */

@@ -30,7 +30,15 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 
 using namespace s3dg;
 
-constexpr int kDefaultOccStream = 14, kDefaultOccBatch = 0;
+constexpr int kDefaultOccStream = 14, kDefaultOccBatch = -1;   // batch: -1 = per launch (below)
+// Batch-kernel occupancy per launch: uncapped (32
+// resident 1-wave workgroups per CU) unless the launch's zero prefixes end on
+// a 64-B line (compress c with 64 % c == 0: c = 2, 4, 8, ... and ratios such
+// as 4/3), where a cap of 30 (29 resident) writes 3-7 % faster: config 3
+// 7214-7260 -> 7416-7424 GB/s, d1 c4 6925 -> 7435, d1 c8 6933 -> 7436, while
+// the same cap costs c = 1, 1.5 and 3 (mid-line prefixes) 2-4 %
+// (profiles/r03/diag/cfg3/power/).
+constexpr int kOccZeroLines = 30;
 constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident workgroups / 64
 constexpr int kDefaultStreamTiles = 1;
 constexpr uint64_t kStreamTilesMinBlocks = 16384;   // smaller streams: 2D kernel, no tile-map launch
@@ -185,11 +193,21 @@ constexpr uint64_t kDefaultBaseSeed = 0xBA5EB10C00000000ull;
     DeviceScope dscope_((c)->device);                                  \
     if (!dscope_.ok()) return hipfail(dscope_.err, "hipSetDevice")
 
-LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false) {
+// A zero prefix that ends on a 64-B line in every block: const_len =
+// 4096 f_num / f_den is a multiple of 64, i.e. 64 f_num / f_den is whole.
+static inline bool zero_line_prefix(uint64_t f_num, uint64_t f_den) {
+    return f_num != 0 && f_den != 0 && (f_num * 64) % f_den == 0;
+}
+
+// zero_lines: the launch's objects (most of its blocks) have line-aligned
+// zero prefixes (zero_line_prefix); picks the batch kernel's occupancy cap
+// when it is not set explicitly (s3dg_set_occupancy).
+LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false, bool zero_lines = false) {
     LaunchCfg lc;
     lc.store = batch ? c->store_batch : c->store_stream;
     lc.waves_per_block = c->waves_per_block ? c->waves_per_block : (batch ? 1 : 2);
-    lc.dyn_lds = occupancy_lds(batch ? c->occ_batch : c->occ_stream, kFillStaticLds);
+    const int occ = !batch ? c->occ_stream : c->occ_batch >= 0 ? c->occ_batch : zero_lines ? kOccZeroLines : 0;
+    lc.dyn_lds = occupancy_lds(occ, kFillStaticLds);
     lc.prefetch_tiles = batch ? c->prefetch_tiles : 0;
     return lc;
 }
@@ -486,7 +504,8 @@ int s3dg_query_keystream_occupancy(s3dg_ctx *c, int mode, int *wgs_per_cu) {
 int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
     CTX_SCOPE(c);
     if (!wgs_per_cu) return fail(S3DG_EINVAL, "null output");
-    HIP_TRY(fill_occupancy(cfg_for(c, batch != 0), batch != 0, wgs_per_cu), "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    HIP_TRY(fill_occupancy(cfg_for(c, batch != 0, batch == 2), batch != 0, wgs_per_cu),
+            "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     return S3DG_OK;
 }
 
@@ -531,7 +550,8 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
         StreamState *S = stream_state(c, s);
         std::lock_guard<std::mutex> g(S->mu);
         if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
-        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
+        const bool zl = pp.f_den != 0 && pp.rem == 0 && pp.floor_len != 0 && (pp.floor_len & 63u) == 0;
+        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true, zl), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
                                           lead, seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s),
                 "launch k_fill_batch(stream)");
         return S3DG_OK;
@@ -720,7 +740,7 @@ private:
 // Pass 1 over descriptors [k0, k1): validation, slot counts per tile size,
 // dense-layout test.
 struct BatchScan {
-    uint64_t m = 0, blocks = 0, ntiles[kTileShiftMax + 1] = {};
+    uint64_t m = 0, blocks = 0, zl_blocks = 0, ntiles[kTileShiftMax + 1] = {};
     uint64_t first_off = 0, last_end = 0;
     bool dense_ok = true;
     int err = S3DG_OK;
@@ -731,8 +751,10 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
                        s3dg_obj_desc *__restrict out) {
     // accumulators in registers (P aliases nothing, but the compiler cannot
     // know that across the staging stores); the checks fold into one flag
-    uint64_t m = 0, blocks = 0, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
+    uint64_t m = 0, blocks = 0, zl_blocks = 0, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
     bool dense = true, bad = false;
+    uint32_t zl_num = 0, zl_den = 1;   // last compress seen and its zero_line_prefix
+    bool zl = false;
     for (uint64_t k = k0; k < k1; ++k) {
         const s3dg_obj_desc o = d[k];
         out[k - k0] = o;   // staged as is; empty objects are squeezed out afterwards (rare)
@@ -745,6 +767,12 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
         dense = dense && (m == 0 || o.dst_off >= last) && (o.dst_off & (kBlk - 1)) == 0;
         last = o.dst_off + nb * kBlk;
         blocks += nb;
+        if (o.f_num != zl_num || o.f_den != zl_den) {
+            zl_num = o.f_num;
+            zl_den = o.f_den;
+            zl = zero_line_prefix(o.f_num, o.f_den);
+        }
+        zl_blocks += zl ? nb : 0;
         ++m;
     }
     if (bad) {   // the first offending descriptor names the error
@@ -760,6 +788,7 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
     }
     P.m = m;
     P.blocks = blocks;
+    P.zl_blocks = zl_blocks;
     P.first_off = first;
     P.last_end = last;
     P.dense_ok = dense;
@@ -774,7 +803,6 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     if (!dst_base || !aligned16(dst_base)) return fail(S3DG_EINVAL, "dst_base must be 16-byte aligned");
     hipStream_t s = (hipStream_t)stream;
     const uintptr_t base = (uintptr_t)dst_base;
-    const LaunchCfg lc = cfg_for(c, true);
     StreamState *S = stream_state(c, s);
     std::lock_guard<std::mutex> g(S->mu);
     if (!S->up) HIP_TRY(hipStreamCreateWithFlags(&S->up, hipStreamNonBlocking), "hipStreamCreate(upload)");
@@ -832,6 +860,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             P.last_end = Q.last_end;
             P.m += Q.m;
             P.blocks += Q.blocks;
+            P.zl_blocks += Q.zl_blocks;
             for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles[sh] += Q.ntiles[sh];
         }
         const uint64_t m = P.m;
@@ -884,7 +913,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         HIP_TRY(hipEventRecord(G.consumed, S->up), "hipEventRecord");
         HIP_TRY(hipEventRecord(S->mapped[tb], S->up), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(s, S->mapped[tb], 0), "hipStreamWaitEvent");
-        LaunchCfg lcs = lc;
+        LaunchCfg lcs = cfg_for(c, true, 2 * P.zl_blocks > P.blocks);
         if (tshift == 0) lcs.store = c->store_dense;
         HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
                 "launch k_fill_batch");

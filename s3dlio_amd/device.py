@@ -196,10 +196,11 @@ class Context:
         call("s3dg_query_keystream_occupancy", self._h, int(mode), ctypes.byref(out))
         return out.value
 
-    def query_occupancy(self, batch: bool = False) -> int:
-        """Resident fill workgroups per CU under the current settings."""
+    def query_occupancy(self, batch: bool = False, zero_lines: bool = False) -> int:
+        """Resident fill workgroups per CU under the current settings (batch
+        launches: `zero_lines` = zero prefixes ending on a 64-B line)."""
         out = ctypes.c_int()
-        call("s3dg_query_occupancy", self._h, 1 if batch else 0, ctypes.byref(out))
+        call("s3dg_query_occupancy", self._h, (2 if zero_lines else 1) if batch else 0, ctypes.byref(out))
         return out.value
 
     # -- generation (asynchronous on `stream`) ----------------------------------

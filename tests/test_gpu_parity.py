@@ -285,13 +285,16 @@ def test_store_modes_and_occupancy_agree(gpu_ctx, torch):
 
 
 def test_occupancy_cap_is_applied(gpu_ctx):
-    # stream default 14 resident 2-wave workgroups per CU, uncapped batch (1 wave)
+    # stream default 14 resident 2-wave workgroups per CU, uncapped batch (1 wave),
+    # 29 for batch launches with line-aligned zero prefixes (cap 30)
     assert gpu_ctx.query_occupancy(batch=False) == 14
-    assert gpu_ctx.query_occupancy(batch=True) >= 16
+    assert gpu_ctx.query_occupancy(batch=True) >= 30
+    assert gpu_ctx.query_occupancy(batch=True, zero_lines=True) == 29
     for cap in (8, 10, 16):
         gpu_ctx.set_occupancy(cap, cap)
         assert gpu_ctx.query_occupancy(batch=False) == cap
         assert gpu_ctx.query_occupancy(batch=True) == cap
+        assert gpu_ctx.query_occupancy(batch=True, zero_lines=True) == cap
     gpu_ctx.set_occupancy(-1, -1)
     assert gpu_ctx.query_occupancy(batch=False) == 14
 

@@ -19,7 +19,7 @@ import variant_lab  # noqa: E402  (library paths only)
 
 MiB = 1 << 20
 POINTS = {"cfg3": (4, 1, 2), "cfg2": (1, 0, 1), "d1c4": (1, 3, 4), "cfg5": (2, 2, 3), "d1c3": (1, 2, 3),
-          "d1c2": (1, 1, 2), "d4c1": (4, 0, 1)}
+          "d1c2": (1, 1, 2), "d4c1": (4, 0, 1), "d2c15": (2, 1, 3), "d1c8": (1, 7, 8), "d1c15": (1, 1, 3)}
 
 
 def points():
@@ -87,7 +87,11 @@ def main():
     print(json.dumps({"smi_device": bdf}), flush=True)
 
     def launch(L, hd, point):
-        d, fn, fd = POINTS[point[1]]
+        name = point[1]
+        if name.startswith("f") and "x" in name:      # "f<f_num>x<f_den>": dedup 1, any compress
+            d, (fn, fd) = 1, map(int, name[1:].split("x"))
+        else:
+            d, fn, fd = POINTS[name]
         r = L.s3dg_fill_controlled_stream(hd, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(d), u32(fn), u32(fd),
                                           u64(0x5EED000000000001), u64(0), sh)
         assert r == 0
@@ -101,7 +105,8 @@ def main():
                 poll["rows"].append({k: m.get(k) for k in ("current_uclk", "current_gfxclk", "current_socket_power",
                                                            "temperature_hbm", "temperature_hotspot",
                                                            "temperature_mem", "average_umc_activity",
-                                                           "throttle_status", "indep_throttle_status")})
+                                                           "throttle_status", "indep_throttle_status", "current_socclk",
+                                                           "voltage_gfx", "voltage_soc", "voltage_mem")})
             except Exception as e:  # noqa: BLE001
                 poll["rows"].append({"error": str(e)})
             time.sleep(0.05)
@@ -148,7 +153,8 @@ def main():
                     out["viol_" + key + "_delta"] = (b - a) if a is not None and b is not None else None
                 rows = [r for r in poll["rows"] if "error" not in r]
                 for key in ("current_uclk", "current_gfxclk", "current_socket_power", "temperature_hbm",
-                            "temperature_hotspot", "temperature_mem", "average_umc_activity"):
+                            "temperature_hotspot", "temperature_mem", "average_umc_activity", "current_socclk",
+                            "voltage_gfx", "voltage_soc", "voltage_mem"):
                     vals = [r[key] for r in rows if isinstance(r.get(key), (int, float))]
                     out[key + "_med"] = statistics.median(vals) if vals else None
                     out[key + "_max"] = max(vals) if vals else None
