@@ -88,6 +88,14 @@ def main():
 
     def launch(L, hd, point):
         name = point[1]
+        if name == "k2":                               # npz keystream, 2 MiB chunks, one launch
+            assert L.s3dg_xoshiro_fill(hd, p, u64(8 * MiB * n), u64(2 * MiB), u64(0), sh) == 0
+            return
+        if name in ("dg1", "dg1c2"):                   # DG1, one launch over the whole buffer
+            d, fn, fd = (2, 1, 2) if name == "dg1c2" else (1, 0, 1)
+            assert L.s3dg_dgen_fill(hd, p, u64(8 * MiB * n), u64(0), u64(1 << 40), u64(d), u32(fn), u32(fd),
+                                    u64(777), sh) == 0
+            return
         if name.startswith("f") and "x" in name:      # "f<f_num>x<f_den>": dedup 1, any compress
             d, (fn, fd) = 1, map(int, name[1:].split("x"))
         else:
