@@ -84,6 +84,13 @@ int s3dg_set_store_policy(s3dg_ctx *ctx, int stream_policy, int batch_policy);
  * line (64 f_num / f_den whole: compress 2, 4, 8, ...).  A tuning knob; results
  * are identical. */
 int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_cu);
+/* Batch kernel (batches and large uniform streams): the stores of each 4 KiB
+ * block wait until `ticks` wall-clock ticks (10 ns) after its workgroup
+ * started; 0 = no floor, negative = per launch (100 when most of the
+ * launch's blocks have a zero prefix of at least half the block that ends
+ * inside a 64-B line, e.g. compress 3; none otherwise).  Measured on MI355X;
+ * results are identical. */
+int s3dg_set_batch_pace(s3dg_ctx *ctx, int ticks);
 /* Batch launches: distance (in units of 64 blocks) at which workgroups warm
  * the L2 with later tile records; 0 = off, UINT32_MAX = default (256).
  * Results are identical. */

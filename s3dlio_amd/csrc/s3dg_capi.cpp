@@ -39,6 +39,15 @@ constexpr int kDefaultOccStream = 14, kDefaultOccBatch = -1;   // batch: -1 = pe
 // the same cap costs c = 1, 1.5 and 3 (mid-line prefixes) 2-4 %
 // (profiles/r03/diag/cfg3/power/).
 constexpr int kOccZeroLines = 30;
+// Zero prefixes of at least half the block that end inside a line (c = 3,
+// 5, 6, 7, ...): uncapped, with the stores held until 100 wall-clock ticks
+// (1 us) after the workgroup starts, whatever the GFX clock (DESIGN.md
+// §5.1.2: config 5 7343 -> 7535-7540 GB/s, d1 c3 7115-7181 -> 7407-7450;
+// config 2 would lose 0.4 %, so prefix-free launches keep no floor).
+constexpr int kDefaultBatchRtFloor = -1;   // per launch
+constexpr uint32_t kRtFloorMidZeros = 100;
+// Launch classes by zero prefix (per launch; batches by majority of blocks)
+enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
 constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident workgroups / 64
 constexpr int kDefaultStreamTiles = 1;
 constexpr uint64_t kStreamTilesMinBlocks = 16384;   // smaller streams: 2D kernel, no tile-map launch
@@ -124,6 +133,7 @@ struct s3dg_ctx {
     // resident fill workgroups per CU (0 = hardware max); measured on MI355X
     // (DESIGN.md §5.1): 14 for 2-wave stream blocks, no cap for 1-wave batch blocks
     int occ_stream = kDefaultOccStream, occ_batch = kDefaultOccBatch;
+    int batch_rt_floor = kDefaultBatchRtFloor;   // batch kernel's wall-clock store floor (ticks; -1 = per launch)
     uint32_t prefetch_tiles = kDefaultPrefetch;   // batch tile-record prefetch distance
     uint32_t tile_shift = 0;           // batch tile = 2^tile_shift blocks; 0 = per launch
     bool tile_force_dense = false;     // batch: one record per 4 KiB granule when the layout allows
@@ -193,21 +203,29 @@ constexpr uint64_t kDefaultBaseSeed = 0xBA5EB10C00000000ull;
     DeviceScope dscope_((c)->device);                                  \
     if (!dscope_.ok()) return hipfail(dscope_.err, "hipSetDevice")
 
-// A zero prefix that ends on a 64-B line in every block: const_len =
-// 4096 f_num / f_den is a multiple of 64, i.e. 64 f_num / f_den is whole.
-static inline bool zero_line_prefix(uint64_t f_num, uint64_t f_den) {
-    return f_num != 0 && f_den != 0 && (f_num * 64) % f_den == 0;
+// Zero-prefix class of compress (f_num, f_den): kZcLines when const_len =
+// 4096 f_num / f_den is a multiple of 64 (64 f_num / f_den whole), i.e. the
+// prefix ends on a 64-B line in every block; kZcMidHeavy when it ends inside
+// a line and covers at least half the block; kZcNone otherwise.
+static inline int zero_class(uint64_t f_num, uint64_t f_den) {
+    if (f_num == 0 || f_den == 0) return kZcNone;
+    if ((f_num * 64) % f_den == 0) return kZcLines;
+    return 2 * f_num >= f_den ? kZcMidHeavy : kZcNone;
 }
 
-// zero_lines: the launch's objects (most of its blocks) have line-aligned
-// zero prefixes (zero_line_prefix); picks the batch kernel's occupancy cap
-// when it is not set explicitly (s3dg_set_occupancy).
-LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false, bool zero_lines = false) {
+// zclass: the launch's zero-prefix class (zero_class; batches: the class of
+// most of its blocks); picks the batch kernel's occupancy cap and store floor
+// when they are not set explicitly (s3dg_set_occupancy, s3dg_set_batch_pace).
+LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false, int zclass = kZcNone) {
     LaunchCfg lc;
     lc.store = batch ? c->store_batch : c->store_stream;
     lc.waves_per_block = c->waves_per_block ? c->waves_per_block : (batch ? 1 : 2);
-    const int occ = !batch ? c->occ_stream : c->occ_batch >= 0 ? c->occ_batch : zero_lines ? kOccZeroLines : 0;
+    const int occ = !batch ? c->occ_stream : c->occ_batch >= 0 ? c->occ_batch
+                                           : zclass == kZcLines ? kOccZeroLines : 0;
     lc.dyn_lds = occupancy_lds(occ, kFillStaticLds);
+    if (batch)
+        lc.rt_floor = c->batch_rt_floor >= 0 ? (uint32_t)c->batch_rt_floor
+                                             : zclass == kZcMidHeavy ? kRtFloorMidZeros : 0u;
     lc.prefetch_tiles = batch ? c->prefetch_tiles : 0;
     return lc;
 }
@@ -444,6 +462,13 @@ int s3dg_set_occupancy(s3dg_ctx *c, int stream_wgs_per_cu, int batch_wgs_per_cu)
     return S3DG_OK;
 }
 
+int s3dg_set_batch_pace(s3dg_ctx *c, int ticks) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (ticks > 100000) return fail(S3DG_EINVAL, "store floor must be at most 100000 ticks (1 ms)");
+    c->batch_rt_floor = ticks < 0 ? kDefaultBatchRtFloor : ticks;
+    return S3DG_OK;
+}
+
 int s3dg_set_batch_prefetch(s3dg_ctx *c, uint32_t tiles) {
     if (!c) return fail(S3DG_EINVAL, "null context");
     c->prefetch_tiles = tiles == UINT32_MAX ? kDefaultPrefetch : tiles;
@@ -504,7 +529,7 @@ int s3dg_query_keystream_occupancy(s3dg_ctx *c, int mode, int *wgs_per_cu) {
 int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
     CTX_SCOPE(c);
     if (!wgs_per_cu) return fail(S3DG_EINVAL, "null output");
-    HIP_TRY(fill_occupancy(cfg_for(c, batch != 0, batch == 2), batch != 0, wgs_per_cu),
+    HIP_TRY(fill_occupancy(cfg_for(c, batch != 0, batch == 2 ? kZcLines : kZcNone), batch != 0, wgs_per_cu),
             "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     return S3DG_OK;
 }
@@ -550,8 +575,12 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
         StreamState *S = stream_state(c, s);
         std::lock_guard<std::mutex> g(S->mu);
         if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
-        const bool zl = pp.f_den != 0 && pp.rem == 0 && pp.floor_len != 0 && (pp.floor_len & 63u) == 0;
-        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true, zl), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
+        // the prefix's class from its exact length (pp: 4096 f_num / f_den = floor_len + rem / f_den)
+        const int zc = pp.f_den == 0 || (pp.floor_len == 0 && pp.rem == 0) ? kZcNone
+                       : pp.rem == 0 && (pp.floor_len & 63u) == 0      ? kZcLines
+                       : 2 * (uint64_t)pp.floor_len >= kBlk            ? kZcMidHeavy
+                                                                        : kZcNone;
+        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true, zc), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
                                           lead, seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s),
                 "launch k_fill_batch(stream)");
         return S3DG_OK;
@@ -740,7 +769,7 @@ private:
 // Pass 1 over descriptors [k0, k1): validation, slot counts per tile size,
 // dense-layout test.
 struct BatchScan {
-    uint64_t m = 0, blocks = 0, zl_blocks = 0, ntiles[kTileShiftMax + 1] = {};
+    uint64_t m = 0, blocks = 0, zc_blocks[3] = {}, ntiles[kTileShiftMax + 1] = {};
     uint64_t first_off = 0, last_end = 0;
     bool dense_ok = true;
     int err = S3DG_OK;
@@ -751,10 +780,10 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
                        s3dg_obj_desc *__restrict out) {
     // accumulators in registers (P aliases nothing, but the compiler cannot
     // know that across the staging stores); the checks fold into one flag
-    uint64_t m = 0, blocks = 0, zl_blocks = 0, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
+    uint64_t m = 0, blocks = 0, zc_blocks[3] = {}, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
     bool dense = true, bad = false;
-    uint32_t zl_num = 0, zl_den = 1;   // last compress seen and its zero_line_prefix
-    bool zl = false;
+    uint32_t zc_num = 0, zc_den = 1;   // last compress seen and its zero_class
+    int zc = kZcNone;
     for (uint64_t k = k0; k < k1; ++k) {
         const s3dg_obj_desc o = d[k];
         out[k - k0] = o;   // staged as is; empty objects are squeezed out afterwards (rare)
@@ -767,12 +796,12 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
         dense = dense && (m == 0 || o.dst_off >= last) && (o.dst_off & (kBlk - 1)) == 0;
         last = o.dst_off + nb * kBlk;
         blocks += nb;
-        if (o.f_num != zl_num || o.f_den != zl_den) {
-            zl_num = o.f_num;
-            zl_den = o.f_den;
-            zl = zero_line_prefix(o.f_num, o.f_den);
+        if (o.f_num != zc_num || o.f_den != zc_den) {
+            zc_num = o.f_num;
+            zc_den = o.f_den;
+            zc = zero_class(o.f_num, o.f_den);
         }
-        zl_blocks += zl ? nb : 0;
+        zc_blocks[zc] += nb;
         ++m;
     }
     if (bad) {   // the first offending descriptor names the error
@@ -788,7 +817,7 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
     }
     P.m = m;
     P.blocks = blocks;
-    P.zl_blocks = zl_blocks;
+    for (int k = 0; k < 3; ++k) P.zc_blocks[k] = zc_blocks[k];
     P.first_off = first;
     P.last_end = last;
     P.dense_ok = dense;
@@ -860,7 +889,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             P.last_end = Q.last_end;
             P.m += Q.m;
             P.blocks += Q.blocks;
-            P.zl_blocks += Q.zl_blocks;
+            for (int k = 0; k < 3; ++k) P.zc_blocks[k] += Q.zc_blocks[k];
             for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles[sh] += Q.ntiles[sh];
         }
         const uint64_t m = P.m;
@@ -913,7 +942,10 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         HIP_TRY(hipEventRecord(G.consumed, S->up), "hipEventRecord");
         HIP_TRY(hipEventRecord(S->mapped[tb], S->up), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(s, S->mapped[tb], 0), "hipStreamWaitEvent");
-        LaunchCfg lcs = cfg_for(c, true, 2 * P.zl_blocks > P.blocks);
+        const int zcls = 2 * P.zc_blocks[kZcLines] > P.blocks      ? kZcLines
+                         : 2 * P.zc_blocks[kZcMidHeavy] > P.blocks ? kZcMidHeavy
+                                                                   : kZcNone;
+        LaunchCfg lcs = cfg_for(c, true, zcls);
         if (tshift == 0) lcs.store = c->store_dense;
         HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
                 "launch k_fill_batch");

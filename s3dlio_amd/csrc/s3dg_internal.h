@@ -71,6 +71,7 @@ struct LaunchCfg {
     uint32_t dyn_lds = 0;  // reserved dynamic LDS per workgroup (occupancy cap)
     uint32_t prefetch_tiles = 0;   // batch: tile-record prefetch distance (0 = off)
     uint32_t pace = 0;             // store-only reference only: wave-0 delay before the stores
+    uint32_t rt_floor = 0;         // batch kernel: wall-clock ticks (10 ns) from workgroup start to its stores
 };
 
 // Dynamic LDS that caps a fill launch at `wgs` resident workgroups per CU

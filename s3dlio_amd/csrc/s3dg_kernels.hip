@@ -303,10 +303,14 @@ __device__ __forceinline__ void store_image(BlockLds &S, uint32_t t, const u32x4
 // ABL: the store-only reference of the same kernel (write ceiling): block
 // geometry, LDS image, barrier and stores as the fill, without the PRNG chain
 // and the window patch phase; its bytes are wrong by design.
+// rt_floor > 0: the block's stores wait until rt_floor wall-clock ticks
+// (100 MHz) after its workgroup started (t0): a floor on the time before the
+// stores that does not scale with the GFX clock.
 template <int NT, int NW, bool IMG = false, bool ABL = false>
 __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, uint32_t wave,
                                           uint32_t i, uint64_t size, uint64_t entropy,
-                                          const PrefixParams &pp, const u32x4 (&B)[4 / NW]) {
+                                          const PrefixParams &pp, const u32x4 (&B)[4 / NW], uint64_t t0 = 0,
+                                          uint32_t rt_floor = 0) {
     constexpr int T = 64 * NW, SPL = 4 / NW;   // segments per lane
     const uint32_t lane = t & 63;
     Plan P;
@@ -322,6 +326,8 @@ __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, 
         __syncthreads();
     }
 #endif
+    if (rt_floor)
+        while (wall_clock64() - t0 < (uint64_t)rt_floor) __builtin_amdgcn_s_sleep(1);
 #if S3DG_DIAG_ZERO & 4
     // diagnostic: pieces stored last-first (the zero prefix's stores after the image's)
 #pragma unroll
@@ -372,6 +378,9 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     __shared__ __attribute__((aligned(16))) BlockLds S;
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    // pace: the store-only reference's wave-0 delay (ABL), else the fill's
+    // wall-clock floor before the stores (rt_floor, 0 = none)
+    const uint64_t t0 = (!ABL && pace) ? wall_clock64() : 0;
     const uint64_t g = g0 + blockIdx.x;
     const uint64_t tile = g >> tshift;
     // The tile record (64 B) in ONE scalar load, issued first; then the base
@@ -394,7 +403,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
         if (wave == 0)
             for (uint32_t q = 0; q < pace; ++q) __builtin_amdgcn_s_sleep(2);
     }
-    gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B);
+    gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B, t0, ABL ? 0u : pace);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
     // 128-byte line (2 records) of the span's records
@@ -897,8 +906,9 @@ void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const u3
 
 template <int NT, int NW>
 void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
-                      uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b, 0u);
+                      uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b, uint32_t rt_floor) {
+    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b,
+                       rt_floor);
 }
 
 template <int NT, int NW>
@@ -1001,7 +1011,7 @@ static hipError_t batch_tiles(const LaunchCfg &lc, uint8_t *dst_base, uint64_t t
                           lc.prefetch_tiles, tshift, b, lc.pace);
         else
             S3DG_DISPATCH(launch_batch_one, lc, dim3(gx), lc.dyn_lds, s, dst_base, tiles, total_tiles, g0,
-                          lc.prefetch_tiles, tshift, b);
+                          lc.prefetch_tiles, tshift, b, lc.rt_floor);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -164,6 +164,12 @@ class Context:
         default); results are identical."""
         call("s3dg_set_occupancy", self._h, int(stream_wgs_per_cu), int(batch_wgs_per_cu))
 
+    def set_batch_pace(self, ticks: int = -1) -> None:
+        """Batch kernel: hold each block's stores until `ticks` wall-clock ticks
+        (10 ns) after its workgroup started (0 = off, negative = per launch);
+        results are identical."""
+        call("s3dg_set_batch_pace", self._h, int(ticks))
+
     def set_batch_prefetch(self, tiles: int = -1) -> None:
         """Tile-record prefetch distance of batch launches in units of 64 blocks
         (0 = off, negative = library default); results are identical."""

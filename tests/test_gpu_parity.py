@@ -284,6 +284,45 @@ def test_store_modes_and_occupancy_agree(gpu_ctx, torch):
     gpu_ctx.set_occupancy(-1, -1)
 
 
+def test_batch_store_floor_identical(gpu_ctx, torch, oracle, base):
+    """The batch kernel's wall-clock store floor (s3dg_set_batch_pace; default
+    100 ticks for mid-line zero prefixes of >= half a block, e.g. compress 3)
+    never changes bytes: a tiled uniform stream and a batch, floors 0..1000."""
+    n, size = 20, 8 * 2**20 + 4096 * 5 + 123          # 20 x 2054 blocks: the tiled batch kernel
+    stride = 8 * 2**20 + 32 * 1024                     # a multiple of 32 KiB: one granule lead
+    ref = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    gpu_ctx.set_batch_pace(0)
+    gpu_ctx.fill_stream(ref, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=11, stride=stride)
+    torch.cuda.synchronize()
+    h = ref.cpu().numpy()
+    for j in (0, n - 1):
+        exp = oracle.fill_controlled(size, 2, 2, 3, P.object_entropy(11, j), base)
+        assert np.array_equal(h[j * stride:j * stride + size], exp), j
+    for ticks in (-1, 1, 100, 1000):
+        gpu_ctx.set_batch_pace(ticks)
+        t = torch.zeros_like(ref)
+        gpu_ctx.fill_stream(t, obj_size=size, n_objs=n, dedup=2, compress=3, seed_base=11, stride=stride)
+        torch.cuda.synchronize()
+        for j in range(n):
+            assert torch.equal(t[j * stride:j * stride + size], ref[j * stride:j * stride + size]), (ticks, j)
+    rnd = random.Random(3)
+    objs, off = [], 0
+    for j in range(60):
+        sz = int(np.exp(rnd.uniform(np.log(4096), np.log(2 * 2**20))))
+        objs.append((off, sz, P.object_entropy(SEED_BASE, j), rnd.choice([1, 2, 4]), rnd.choice([3, 3, 5, 2, 1])))
+        off += (sz + 16 + 4095) // 4096 * 4096
+    for ticks in (-1, 0, 300):
+        gpu_ctx.set_batch_pace(ticks)
+        out = torch.full((off,), GUARD, dtype=torch.uint8, device="cuda")
+        gpu_ctx.fill_batch(out, objs)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for (o, sz, e, d, c) in objs:
+            fn, fd = P.compress_ratio(c)
+            assert np.array_equal(got[o:o + sz], oracle.fill_controlled(sz, d, fn, fd, e, base)), (ticks, o)
+    gpu_ctx.set_batch_pace(-1)
+
+
 def test_occupancy_cap_is_applied(gpu_ctx):
     # stream default 14 resident 2-wave workgroups per CU, uncapped batch (1 wave),
     # 29 for batch launches with line-aligned zero prefixes (cap 30)

@@ -23,11 +23,13 @@ POINTS = {"cfg3": (4, 1, 2), "cfg2": (1, 0, 1), "d1c4": (1, 3, 4), "cfg5": (2, 2
 
 
 def points():
-    """LAB_POINTS="cfg3,cfg2,cfg3@28": name[@batch workgroups per CU cap]."""
+    """LAB_POINTS="cfg3,cfg2,cfg3@28,cfg5@0%100": name[@batch workgroups per CU
+    cap][%batch store floor in wall-clock ticks]; omitted = library default."""
     out = []
     for item in os.environ.get("LAB_POINTS", "cfg3,cfg2,d1c4").split(","):
-        name, _, occ = item.partition("@")
-        out.append((item, name, int(occ) if occ else -1))
+        head, _, pace = item.partition("%")
+        name, _, occ = head.partition("@")
+        out.append((item, name, int(occ) if occ else -1, int(pace) if pace else -1))
     return out
 
 
@@ -120,12 +122,14 @@ def main():
             time.sleep(0.05)
 
     for name, (L, hd) in libs.items():        # warm both builds
-        launch(L, hd, ("cfg2", "cfg2", -1))
+        launch(L, hd, ("cfg2", "cfg2", -1, -1))
     torch.cuda.synchronize()
     for rep in range(reps):
         for point in points():
             for name, (L, hd) in libs.items():
                 assert L.s3dg_set_occupancy(hd, -1, point[2]) == 0
+                if hasattr(L, "s3dg_set_batch_pace"):
+                    assert L.s3dg_set_batch_pace(hd, point[3]) == 0
                 m0, v0 = metrics(smi, h)
                 poll["on"], poll["rows"] = True, []
                 th = threading.Thread(target=poller)
