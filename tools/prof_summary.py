@@ -42,8 +42,13 @@ def main(src, rnd):
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    traffic = {}
     digest = bench.source_digest()
+    # keep records of other configs taken at the same library digest (several
+    # profile directories per round); records of older digests are dropped
+    try:
+        traffic = {k: v for k, v in json.load(open(tpath)).items() if v.get("source_digest") == digest}
+    except (OSError, ValueError):
+        traffic = {}
     try:
         commit = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], text=True).strip()
     except Exception:
