@@ -3,7 +3,7 @@ checked byte for byte against the C oracle (oracle/s3dg_oracle.c), with guard
 bytes around every output.  Complements the fixed edge-case fixtures: random
 sizes (ragged tails, 1..7-byte tails, block and chunk boundaries), dedup
 factors, integer and rational compress ratios, entropies near 2^64, random
-base blocks and random launch knobs (waves, occupancy, store policy,
+base blocks and random launch knobs (waves, occupancy, store floor, store policy,
 prefetch, batch tile size, keystream shape).  Reference semantics: src/data_gen.rs:151-224
 (fill), :102-132 (random-data layout), src/data_formats/npz.rs:376-383 (K2).
 """
@@ -47,6 +47,7 @@ def _knobs(ctx, rnd):
     ctx.set_store_policy(sp, sp)
     ctx.set_batch_prefetch(rnd.choice([-1, 0, 1, 7, 128, 256, 1 << 20]))
     ctx.set_batch_tile(rnd.choice([0, 0, 1, 2, 4, 8, 16, 32, 64]))
+    ctx.set_batch_pace(rnd.choice([-1, -1, 0, 50, 200]))   # wall-clock store floor (per-launch default: -1)
 
 
 def _reset(ctx):
@@ -55,6 +56,7 @@ def _reset(ctx):
     ctx.set_store_policy(-1, -1)
     ctx.set_batch_prefetch(-1)
     ctx.set_batch_tile(0)
+    ctx.set_batch_pace(-1)
     ctx.set_stream_tiles(-1)
     ctx.set_keystream_shape(0)
     ctx.set_keystream_shape(1)
