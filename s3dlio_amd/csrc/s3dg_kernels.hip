@@ -326,8 +326,12 @@ __device__ __forceinline__ void gen_block(uint8_t *bd, BlockLds &S, uint32_t t, 
         __syncthreads();
     }
 #endif
+    // bounded as well by sleep count (4 x rt_floor sleeps of >= 64 cycles, i.e.
+    // at least rt_floor x 256 cycles), so the wait ends even if the real-time
+    // counter did not advance
     if (rt_floor)
-        while (wall_clock64() - t0 < (uint64_t)rt_floor) __builtin_amdgcn_s_sleep(1);
+        for (uint32_t n = 0; n < 4 * rt_floor && wall_clock64() - t0 < (uint64_t)rt_floor; ++n)
+            __builtin_amdgcn_s_sleep(1);
 #if S3DG_DIAG_ZERO & 4
     // diagnostic: pieces stored last-first (the zero prefix's stores after the image's)
 #pragma unroll
