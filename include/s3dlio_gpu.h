@@ -131,6 +131,11 @@ int s3dg_query_occupancy(s3dg_ctx *ctx, int batch, int *wgs_per_cu);
 /* ---- parameter helpers (host math shared with the kernels) --------------- */
 uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup);
 int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
+/* Launch class of compress (f_num, f_den) for the batch kernel's per-launch
+ * settings: 1 = zero prefix ending on a 64-B line (cap 30),
+ * 2 = zero prefix of at least half the block ending inside a line (store
+ * floor 100 ticks), 0 = otherwise, or f_den = 0 (no cap, no floor). */
+int s3dg_zero_class(uint32_t f_num, uint32_t f_den);
 /* Per-object entropy of object j of a stream: seed_base + j * 2^32. */
 uint64_t s3dg_object_entropy(uint64_t seed_base, uint64_t j);
 

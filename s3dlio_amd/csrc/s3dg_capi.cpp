@@ -296,6 +296,8 @@ uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup) {
     return (uint64_t)r;
 }
 
+int s3dg_zero_class(uint32_t f_num, uint32_t f_den) { return zero_class(f_num, f_den); }
+
 int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den) {
     if (!f_num || !f_den) return fail(S3DG_EINVAL, "null output");
     if (compress > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "compress must fit in 32 bits");

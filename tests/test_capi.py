@@ -54,6 +54,23 @@ def test_host_helpers_match_oracle():
         assert object_entropy(0x5EED000000000001, j) == P.object_entropy(0x5EED000000000001, j)
 
 
+def test_zero_class_rule():
+    """The batch kernel's per-launch class: 1 = zero prefix
+    ending on a 64-B line (occupancy cap), 2 = >= half a block ending inside a
+    line (wall-clock store floor), 0 = neither.  Pure host math."""
+    from s3dlio_amd._lib import lib
+    from s3dlio_amd import compress_ratio
+    cls = lambda c: lib.s3dg_zero_class(*compress_ratio(c))
+    assert [cls(c) for c in (1, 2, 4, 8, 16, 32, 64)] == [0, 1, 1, 1, 1, 1, 1]
+    assert [cls(c) for c in (3, 5, 6, 7, 9, 100)] == [2, 2, 2, 2, 2, 2]
+    assert cls((3, 2)) == 0 and cls((5, 3)) == 0 and cls((4, 3)) == 1 and cls((8, 3)) == 1 and cls((7, 3)) == 2
+    assert lib.s3dg_zero_class(0, 1) == 0 and lib.s3dg_zero_class(1, 0) == 0
+    for fn, fd in [(1, 2), (3, 4), (2, 3), (1, 3), (2, 5), (1, 4), (4, 5), (63, 64), (127, 128)]:
+        prefix = 4096 * fn / fd
+        want = 1 if prefix % 64 == 0 else (2 if prefix >= 2048 else 0)
+        assert lib.s3dg_zero_class(fn, fd) == want, (fn, fd)
+
+
 def test_no_gpu_is_an_error_not_a_fallback():
     import torch
     if torch.cuda.is_available():
