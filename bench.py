@@ -135,6 +135,8 @@ def parse():
     p.add_argument("--prefetch", type=int, default=None,
                    help="batch tile-record prefetch distance in 64-block units (default: library's, 256)")
     p.add_argument("--batch-tile", type=int, default=None, help="batch tile blocks (1 = dense; default: per launch)")
+    p.add_argument("--pace", type=int, default=None,
+                   help="batch kernel wall-clock store floor in 10-ns ticks (0 = off; default: per launch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-d2h", action="store_true")
@@ -239,6 +241,8 @@ def main() -> int:
         ctx.set_batch_prefetch(args.prefetch)
     if args.batch_tile is not None:
         ctx.set_batch_tile(args.batch_tile)
+    if args.pace is not None:
+        ctx.set_batch_pace(args.pace)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     fn, fd = compress_ratio(cfg["compress"])
