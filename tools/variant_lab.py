@@ -54,6 +54,7 @@ def main():
     from s3dlio_amd._lib import ObjDesc
     MiB = 1 << 20
     n = int(os.environ.get("LAB_N", "10000"))
+    nsmall = int(os.environ.get("LAB_NSMALL", str(20 * n)))   # objects of the kb20* kinds
     u64, u32 = ctypes.c_uint64, ctypes.c_uint32
     libs = {}
     for name in variants():
@@ -67,12 +68,15 @@ def main():
                                    ("small", log_uniform_sizes(10 * n, 5, 4096, MiB), 1, 0, 1),
                                    ("mid", [MiB + 123] * (5 * n), 3, 2, 3),
                                    ("kb64", [64 << 10] * (10 * n), 1, 0, 1),
-                                   ("kb20", [(20 << 10) + 5] * (20 * n), 1, 0, 1)]:
+                                   ("kb20", [(20 << 10) + 5] * nsmall, 1, 0, 1),
+                                   ("kb20n", [20 << 10] * nsmall, 1, 0, 1),      # 5 blocks, packed
+                                   ("kb20g", [20 << 10] * nsmall, 1, 0, 1)]:     # 5 blocks, 24 KiB stride
+        gap = 4096 if kind == "kb20g" else 0
         arr = (ObjDesc * len(sizes))()
         off = 0
         for j, sz in enumerate(sizes):
             arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), d, fn, fd)
-            off += (sz + 4095) // 4096 * 4096
+            off += (sz + 4095) // 4096 * 4096 + gap
         descs[kind] = (arr, sum(sizes), off)
     crcs = {}
     work = {"stream2": 8 * MiB * n, "k2": 8 * MiB * n, "k2_8g": 8 * MiB * n, "dg1": 8 * MiB * n,
