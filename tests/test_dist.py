@@ -40,7 +40,7 @@ def _worker(rank, world, port, n_total, size, q):
     cp.close()
 
 
-@pytest.mark.parametrize("n_total,world", [(7, 2), (64, 2), (37, 4)])
+@pytest.mark.parametrize("n_total,world", [(7, 2), (64, 2), (37, 4), (83, 8)])
 def test_two_rank_sharding_matches_single_stream(oracle, n_total, world):
     size = 4096 * 3 + 100
     ctx = mp.get_context("spawn")
