@@ -30,6 +30,9 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 
 using namespace s3dg;
 
+#ifndef S3DG_DIAG_OLDTILECOST
+#define S3DG_DIAG_OLDTILECOST 0   // diagnostic builds only: the first cost model's tile size (A/B)
+#endif
 constexpr int kDefaultOccStream = 14, kDefaultOccBatch = -1;   // batch: -1 = per launch (below)
 // Batch-kernel occupancy per launch: uncapped (32
 // resident 1-wave workgroups per CU) unless the launch's zero prefixes end on
@@ -706,6 +709,14 @@ constexpr uint64_t kBatchSubFirst = 16384, kBatchSubMax = 262144;
 // to forced dense / 8-block layouts of uniform 7..26-block objects with the
 // dense launches' nt sc1 stores (profiles/r02/diag/batch_lab_store_cost.log)
 constexpr double kDeadSlotCost = 0.4, kRecordCost = 0.05;
+// Among tile sizes, the costs measured on config 4's mixed sizes (forced 64 /
+// 32 / 16 / 8-block tiles: 7249 / 7215 / 7152 / 6991 GB/s, one process,
+// profiles/r03/diag/cfg4/cfg4_tiles.log) fit a dead slot at ~0 and a record at
+// ~0.25 live blocks: a tile's dead slots find its record already in the
+// scalar cache, while each extra record is one more miss on a workgroup's
+// critical path.  The first model (above) picked 16-block tiles there; it
+// still decides dense vs tiled, as fitted.
+constexpr double kDeadSlotCostTiled = 0.1, kRecordCostTiled = 0.25;
 constexpr int kPrepParts = 8;                   // host threads per sub-batch pass
 constexpr uint64_t kPrepMinPerPart = 8192;      // descriptors below which a pass stays single-threaded
 
@@ -903,11 +914,20 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         if (c->tile_shift == 0 && c->tile_force_dense && P.dense_ok) tshift = 0;
         else if (c->tile_shift) tshift = c->tile_shift;
         else {
-            double best = 1e300;
+            // tile size by the tiled costs; dense vs the first model's best tiling by the first model
+            double best = 1e300, best_t = 1e300;
             for (uint32_t sh = kTileShiftMax; sh >= kTileShiftAutoMin; --sh) {
-                const double cost =
-                    kDeadSlotCost * (double)((P.ntiles[sh] << sh) - P.blocks) + kRecordCost * (double)P.ntiles[sh];
-                if (cost < best) { best = cost; tshift = sh; }
+                const double dead = (double)((P.ntiles[sh] << sh) - P.blocks), recs = (double)P.ntiles[sh];
+                const double cost = kDeadSlotCost * dead + kRecordCost * recs;
+                const double cost_t = kDeadSlotCostTiled * dead + kRecordCostTiled * recs;
+                const bool better = cost < best;
+                if (better) best = cost;
+#if S3DG_DIAG_OLDTILECOST
+                if (better) tshift = sh;   // diagnostic: the first model's tile choice
+#else
+                (void)better;
+                if (cost_t < best_t) { best_t = cost_t; tshift = sh; }
+#endif
             }
             if (P.dense_ok && kDeadSlotCost * (double)(span - P.blocks) + kRecordCost * (double)span < best)
                 tshift = 0;

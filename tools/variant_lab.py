@@ -65,6 +65,11 @@ def main():
     descs = {}
     for kind, sizes, d, fn, fd in [("cfg4", log_uniform_sizes(n), 2, 1, 3), ("cfg7", [8 * MiB] * n, 1, 0, 1),
                                    ("cfg4d1", log_uniform_sizes(n), 1, 0, 1), ("cfg4c1", log_uniform_sizes(n), 2, 0, 1),
+                                   # config 4's sizes rounded up to whole 64-block tiles (256 KiB): no dead slots
+                                   ("cfg4r", [(x + (256 << 10) - 1) // (256 << 10) * (256 << 10) for x in log_uniform_sizes(n)],
+                                    1, 0, 1),
+                                   # config 4's sizes, largest first / smallest first
+                                   ("cfg4desc", sorted(log_uniform_sizes(n), reverse=True), 1, 0, 1),
                                    ("small", log_uniform_sizes(10 * n, 5, 4096, MiB), 1, 0, 1),
                                    ("mid", [MiB + 123] * (5 * n), 3, 2, 3),
                                    ("kb64", [64 << 10] * (10 * n), 1, 0, 1),
@@ -133,7 +138,10 @@ def main():
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "4"))):
         for pt in pts:
-            for name, (L, h) in libs.items():
+            order = list(libs.items())
+            if os.environ.get("LAB_ALTERNATE") and rep % 2:   # reverse the variant order on odd rounds
+                order.reverse()
+            for name, (L, h) in order:
                 k, w, o, f, sp, tb = pt
                 assert L.s3dg_set_waves_per_block(h, w) == 0
                 assert L.s3dg_set_occupancy(h, o, o) == 0
