@@ -321,6 +321,9 @@ def test_batch_store_floor_identical(gpu_ctx, torch, oracle, base):
             fn, fd = P.compress_ratio(c)
             assert np.array_equal(got[o:o + sz], oracle.fill_controlled(sz, d, fn, fd, e, base)), (ticks, o)
     gpu_ctx.set_batch_pace(-1)
+    with pytest.raises(Exception):
+        gpu_ctx.set_batch_pace(100001)          # more than 1 ms per block is refused
+    gpu_ctx.set_batch_pace(-1)
 
 
 def test_occupancy_cap_is_applied(gpu_ctx):
