@@ -21,7 +21,9 @@ DG1 byte path behind generate_data / Generator (one launch per object), 16/17
 the same objects through s3dg_dgen_fill_stream (one launch per step), 18-22
 the host-buffer drop-ins (the reference's own API: s3dlio_fill_controlled_data
 on 1/4/16 MiB and 1 GiB host buffers from a native loop, generate_into_buffer
-from 8 threads; --host-mem pageable|pinned; roofline bound = PCIe).
+from 8 threads; --host-mem pageable|pinned; roofline bound = PCIe), 23-28 the
+reference's streaming callers (ObjectGen::fill_chunk at 64 KiB / 256 KiB /
+32 MiB over 8 MiB and 1 GiB objects from 8 threads).
 --d2h-full: the D2H-inclusive rate over the rank's whole object range (config 5
 as BASELINE states it), not an 8 GiB sample.
 
@@ -97,6 +99,22 @@ CONFIGS = {
              kind="host", n=8, size=1 * GiB, dedup=1, compress=1, scaling="weak"),
     22: dict(name="host: generate_into_buffer (s3dg_generate_data) from 8 threads, 8 MiB each, 100 calls per thread",
              kind="host", n=100, size=8 * MiB, threads=8, dedup=1, compress=1, scaling="weak"),
+    # the reference's streaming callers: ObjectGen::fill_chunk loops from 8 threads, one generator per object
+    23: dict(name="chunks: ObjectGen::fill_chunk(64 KiB) over 8 MiB objects, 8 threads x 100 objects "
+                  "(StreamingDataWriter::generate_remaining)", kind="host", n=100, size=8 * MiB, chunk=64 * KiB,
+             threads=8, dedup=1, compress=1, scaling="weak"),
+    24: dict(name="chunks: ObjectGen::fill_chunk(256 KiB) over 8 MiB objects, 8 threads x 100 objects "
+                  "(Config::chunk_size)", kind="host", n=100, size=8 * MiB, chunk=256 * KiB, threads=8, dedup=1,
+             compress=1, scaling="weak"),
+    25: dict(name="chunks: ObjectGen::fill_chunk(32 MiB) over 8 MiB objects, 8 threads x 100 objects "
+                  "(fill_remaining)", kind="host", n=100, size=8 * MiB, chunk=32 * MiB, threads=8, dedup=1,
+             compress=1, scaling="weak"),
+    26: dict(name="chunks: ObjectGen::fill_chunk(64 KiB) over 1 GiB objects, 8 threads x 1 object", kind="host",
+             n=1, size=1 * GiB, chunk=64 * KiB, threads=8, dedup=1, compress=1, scaling="weak"),
+    27: dict(name="chunks: ObjectGen::fill_chunk(256 KiB) over 1 GiB objects, 8 threads x 1 object", kind="host",
+             n=1, size=1 * GiB, chunk=256 * KiB, threads=8, dedup=1, compress=1, scaling="weak"),
+    28: dict(name="chunks: ObjectGen::fill_chunk(32 MiB) over 1 GiB objects, 8 threads x 1 object", kind="host",
+             n=1, size=1 * GiB, chunk=32 * MiB, threads=8, dedup=1, compress=1, scaling="weak"),
 }
 PCIE_PEAK_GBS = 63.0    # PCIe Gen5 x16, one direction, before protocol overhead
 
@@ -158,18 +176,15 @@ def sha(b) -> str:
 
 
 def source_digest() -> str:
-    """Digest of the library sources the measured kernels are built from: a
-    traffic record (profiles/traffic.json) counts only for the same digest."""
-    h = hashlib.sha256()
-    csrc = os.path.join(ROOT, "s3dlio_amd", "csrc")
-    for name in sorted(os.listdir(csrc)):
-        if name.endswith((".hip", ".cpp", ".h", ".c")):
-            with open(os.path.join(csrc, name), "rb") as f:
-                h.update(name.encode() + b"\0" + f.read())
-    for extra in ("include/s3dlio_gpu.h", "s3dlio_amd/build.py"):
-        with open(os.path.join(ROOT, extra), "rb") as f:
-            h.update(extra.encode() + b"\0" + f.read())
-    return h.hexdigest()[:16]
+    """Digest of the library sources in this tree (s3dlio_amd/build.py's
+    source_digest, loaded by path so the package is not imported): the
+    library compiles the same digest in (s3dg_build_digest), and a traffic
+    record (profiles/traffic.json) counts only for the same digest."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_s3dg_build", os.path.join(ROOT, "s3dlio_amd", "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_digest()
 
 
 def cpu_share() -> dict:
@@ -225,6 +240,13 @@ def main() -> int:
     from s3dlio_amd._lib import ObjDesc, call, lib
     from s3dlio_amd.shard import ControlPlane, object_range
 
+    # the timed binary must be the one these sources build
+    lib_digest = (lib.s3dg_build_digest() or b"").decode()
+    src_digest = source_digest()
+    if lib_digest != src_digest:
+        print(f"bench: the loaded library ({lib._name}) was built from sources {lib_digest}, this tree is "
+              f"{src_digest}: rebuild (python s3dlio_amd/build.py) before measuring", file=sys.stderr)
+        return 3
     cp = ControlPlane()
     rank, world = cp.rank, cp.world
     dev = cp.local_rank if args.device_override is None else args.device_override
@@ -336,9 +358,24 @@ def main() -> int:
         u64, vp = ctypes.c_uint64, ctypes.c_void_p
         nl.nl_host_fill_loop.argtypes = [vp, vp, u64, u64, u64, u64]
         nl.nl_threads_gen_loop.argtypes = [vp, ctypes.POINTER(vp), u64, ctypes.c_int, u64, u64, u64]
-        hbufs = [host_buffer(size, args.host_mem, call) for _ in range(nthr)]
+        chunk = cfg.get("chunk")
+        hbufs = [host_buffer(chunk or size, args.host_mem, call) for _ in range(nthr)]
         ring = None
-        if nthr == 1:
+        if chunk:
+            nl.nl_threads_chunk_loop.argtypes = [vp, vp, vp, ctypes.POINTER(vp), ctypes.c_int, u64, u64, u64, u64,
+                                                 u64, u64, ctypes.POINTER(u64)]
+            fns = [ctypes.cast(getattr(lib, f), vp) for f in ("s3dg_gen_create", "s3dg_gen_fill_chunk",
+                                                               "s3dg_gen_destroy")]
+            arr = (vp * nthr)(*[b for b, _ in hbufs])
+            made = ctypes.c_uint64()
+
+            def host_step():
+                r = nl.nl_threads_chunk_loop(*fns, arr, nthr, size, chunk, calls, d, cfg["compress"], SEED_BASE,
+                                             ctypes.byref(made))
+                if r or made.value != nthr * calls * size:
+                    raise RuntimeError(f"fill_chunk loop failed ({r}, {made.value} bytes): "
+                                       f"{lib.s3dg_last_error().decode()}")
+        elif nthr == 1:
             fptr = ctypes.cast(lib.s3dlio_fill_controlled_data, vp)
 
             def host_step(b=hbufs[0][0]):
@@ -384,7 +421,15 @@ def main() -> int:
     tiled = (kind == "stream" and args.stream_tiles != 0
              and all(b // cfg["size"] * ((cfg["size"] + 4095) // 4096) >= 16384 for _, b in launches)
              and cfg["size"] % (32 * KiB) == 0)
-    if kind == "host":
+    if kind == "host" and cfg.get("chunk"):
+        kernel, launch_shape = (
+            "k_keystream (DG1) into the generators' pinned read-ahead rings (chunks below a ring half) or "
+            "+ hipMemcpyAsync D2H on the host slots' staging streams (larger chunks)"), (
+            f"{cfg['threads']} caller threads, one generator per {cfg['size'] // MiB} MiB object, "
+            f"fill_chunk({cfg['chunk'] // KiB} KiB) into a reused {args.host_mem} buffer per thread, slots "
+            f"{os.environ.get('S3DLIO_GPU_DEVICES') or os.environ.get('S3DLIO_GPU_DEVICE') or 'every visible GPU'}, "
+            f"ring half {os.environ.get('S3DLIO_GEN_RING_HALF_MIB', '4')} MiB")
+    elif kind == "host":
         kernel, launch_shape = ("k_fill_stream + hipMemcpyAsync D2H on the host slots' staging streams"
                                 if cfg.get("threads", 1) == 1 else
                                 "k_keystream (DG1) + hipMemcpyAsync D2H on the host slots' staging streams"), (
@@ -445,6 +490,9 @@ def main() -> int:
     algo_per_launch = int(sum(launch_bytes) / len(launch_bytes))
     if kind in ("single", "host"):
         algo_per_launch = cfg["size"]
+    if kind == "host" and cfg.get("chunk"):   # one "call" = one fill_chunk
+        avg_ms = avg_ms * min(cfg["chunk"], cfg["size"]) / cfg["size"]
+        algo_per_launch = min(cfg["chunk"], cfg["size"])
 
     total_bytes = cp.sum(step_bytes) * args.steps
     value = total_bytes / elapsed / GiB
@@ -504,7 +552,7 @@ def main() -> int:
                     "frac": round(achieved_gbs / PCIE_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
                     "launch_shape": launch_shape, "avg_call_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_call": algo_per_launch, "host_mem": args.host_mem,
-                    "source_digest": source_digest()}
+                    "source_digest": src_digest, "library_digest": lib_digest}
         else:
             roof = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
@@ -512,7 +560,7 @@ def main() -> int:
                     "kernel": kernel, "launch_shape": launch_shape,
                     "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": algo_per_launch,
-                    "source_digest": source_digest()}
+                    "source_digest": src_digest, "library_digest": lib_digest}
         if ceil:
             roof.update(ceil)
             roof["frac_of_store_only_best"] = round(achieved_gbs / ceil["store_only_best_GBps"], 4)
@@ -571,6 +619,28 @@ def verify_host(hbufs, cfg, fn, fd, call, cp) -> bool:
     from oracle import oracle_c as OC
     size = cfg["size"]
     b = hbufs[0][0]
+    if cfg.get("chunk"):
+        # thread 0's last fill_chunk holds the tail of its last object (seed SEED_BASE + calls - 1); and one
+        # whole object re-made through the same chunk size, both vs the DG1 oracle
+        chunk, calls = cfg["chunk"], cfg["n"]
+        tail = size % chunk or min(chunk, size)
+        got = np.ctypeslib.as_array((ctypes.c_uint8 * tail).from_address(b))
+        exp = OC.dgen_fill(size, cfg["dedup"], fn, fd, SEED_BASE + calls - 1)
+        ok = sha(got) == sha(exp[size - tail:])
+        n1 = min(size, 64 * MiB)
+        g = ctypes.c_void_p()
+        call("s3dg_gen_create", n1, cfg["dedup"], cfg["compress"], 1, 7, ctypes.byref(g))
+        out = np.empty(n1, np.uint8)
+        w, pos = ctypes.c_uint64(), 0
+        while pos < n1:
+            call("s3dg_gen_fill_chunk", g, out.ctypes.data + pos, min(chunk, n1 - pos), ctypes.byref(w))
+            pos += w.value
+        call("s3dg_gen_destroy", g)
+        ok &= sha(out) == sha(OC.dgen_fill(n1, cfg["dedup"], fn, fd, 7))
+        verified = bool(cp.max(0.0 if ok else 1.0) == 0.0)
+        if not verified:
+            print("bench: VERIFICATION FAILED: fill_chunk output differs from the oracle", file=sys.stderr)
+        return verified
     got = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(b))
     if cfg.get("threads", 1) == 1:
         call("s3dlio_fill_controlled_data_seeded", b, size, cfg["dedup"], cfg["compress"], 7, None)
@@ -901,6 +971,17 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes):
                                     base.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
             return pos + (sz + 4095) // 4096 * 4096, sz
         what = "objects of the config's sizes, one object per task"
+    elif kind == "host" and cfg.get("chunk"):
+        # the same loop on the CPU: 8 threads streaming DG1 objects chunk by chunk (PRNG state carried across
+        # chunks, s3dgo_dgen_stream_fill) into a reused chunk buffer each
+        nthr = cfg["threads"]
+        chunk = min(cfg["chunk"], cfg["size"])
+        b, dt = OC.dgen_chunk_bench(nthr, cfg["size"], chunk, cfg["dedup"], fn, fd, SEED_BASE, seconds)
+        meta["cores"] = nthr
+        return dict(meta, value=round(b / dt / GiB, 2), unit="GiB/s",
+                    sample=f"{b / GiB:.1f} GiB of {cfg['size'] // MiB} MiB DG1 objects as {chunk // KiB} KiB "
+                           f"fill_chunk calls over {dt:.1f} s on {nthr} threads (streaming port, one object "
+                           f"at a time per thread); {cpu_model()}")
     elif kind == "host":     # generate_into_buffer from several threads: DG1 objects, one per call
         ring, nthr = cfg["size"], cfg["threads"]
         threads = nthr

@@ -378,6 +378,10 @@ int s3dlio_fill_controlled_data_seeded(uint8_t *buf, size_t len, size_t dedup,
 
 const char *s3dg_last_error(void);
 const char *s3dg_version(void);
+/* The 16-hex-digit digest of the sources the library was built from
+ * (s3dlio_amd/build.py source_digest); bench.py stamps it and refuses a
+ * library whose digest differs from the tree it runs in. */
+const char *s3dg_build_digest(void);
 
 #pragma GCC visibility pop
 

@@ -289,6 +289,13 @@ pub struct DataGenerator {
 // The library serialises calls on one handle; a generator may move threads
 // (the PyO3 Generator calls it under py.detach).
 unsafe impl Send for DataGenerator {}
+// Sync: pyo3 ^0.27 (Cargo.toml:99) requires every #[pyclass] to be Sync
+// (assert_pyclass_sync), and PyGenerator holds a DataGenerator.  Sound: every
+// s3dg_gen_* call that reads or moves the stream position takes the handle's
+// own mutex (s3dg_generator.cpp, s3dg_gen::mu), the &self accessors
+// (is_complete, position, total_size, seed) read a position the library keeps
+// atomic, and the only mutators here take &mut self.
+unsafe impl Sync for DataGenerator {}
 
 impl DataGenerator {
     pub fn try_new(config: GeneratorConfig) -> anyhow::Result<Self> {

@@ -59,6 +59,12 @@ def lib():
         L.s3dgo_xoshiro_chunks.argtypes = [u8p, u64, u64, u64]
         L.s3dgo_dgen_fill.argtypes = [u8p, u64, u64, u64, u64, u64]
         L.s3dgo_random_data.argtypes = [u8p, u64, u64, u8p]
+        L.s3dgo_dgen_stream_init.argtypes = [ctypes.c_void_p, u64, u64, u64, u64, u64]
+        L.s3dgo_dgen_stream_fill.argtypes = [ctypes.c_void_p, u8p, u64]
+        L.s3dgo_dgen_stream_fill.restype = u64
+        L.s3dgo_dgen_chunk_bench.argtypes = [ctypes.c_int, u64, u64, u64, u64, u64, u64, ctypes.c_double,
+                                             ctypes.POINTER(ctypes.c_double)]
+        L.s3dgo_dgen_chunk_bench.restype = u64
         _lib = L
     return _lib
 
@@ -149,3 +155,27 @@ def random_data(size: int, entropy: int, base: np.ndarray) -> np.ndarray:
     base = np.ascontiguousarray(base, np.uint8)
     lib().s3dgo_random_data(_ptr(out), size, entropy & (2**64 - 1), _ptr(base))
     return out
+
+
+def dgen_stream(size: int, dedup: int, f_num: int, f_den: int, seed: int, chunk: int) -> np.ndarray:
+    """DG1 produced chunk by chunk by the CPU streaming port (s3dgo_dgen_stream_fill)."""
+    st = (ctypes.c_uint64 * 16)()
+    lib().s3dgo_dgen_stream_init(st, size, dedup, f_num, f_den, seed & (2**64 - 1))
+    out = np.empty(size, np.uint8)
+    pos = 0
+    while pos < size:
+        w = lib().s3dgo_dgen_stream_fill(st, ctypes.cast(out.ctypes.data + pos, ctypes.POINTER(ctypes.c_uint8)),
+                                         chunk)
+        if w == 0:
+            break
+        pos += w
+    return out
+
+
+def dgen_chunk_bench(threads: int, obj_size: int, chunk: int, dedup: int, f_num: int, f_den: int,
+                     seed_base: int, seconds: float) -> tuple[int, float]:
+    """(bytes, elapsed s) of `threads` CPU threads streaming DG1 objects chunk by chunk."""
+    el = ctypes.c_double()
+    b = lib().s3dgo_dgen_chunk_bench(threads, obj_size, chunk, dedup, f_num, f_den, seed_base & (2**64 - 1),
+                                     seconds, ctypes.byref(el))
+    return b, el.value

@@ -22,12 +22,14 @@
  * (src/data_gen.rs:192-195) and the 4 KiB A_BASE_BLOCK from ThreadRng
  * (src/constants.rs:715-720).  Both are parameters here.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdatomic.h>
+#include <time.h>
 
 #define S3DGO_BLK 4096u        /* BLK_SIZE   src/constants.rs:326 */
 #define S3DGO_HALF 2048u       /* HALF_BLK   src/constants.rs:329 */
@@ -356,4 +358,120 @@ void s3dgo_random_data(uint8_t *buf, uint64_t size, uint64_t entropy, const uint
         s3dgo_fill_bytes(s, buf + off, bs < S3DGO_MOD ? bs : S3DGO_MOD);
         if (bs > S3DGO_HALF) s3dgo_fill_bytes(s, buf + off + bs - S3DGO_MOD, S3DGO_MOD);
     }
+}
+
+/* ---- DG1 chunked streaming on the CPU (the CPU baseline of bench.py's
+ * fill_chunk configs; test infrastructure) ----------------------------------
+ * The same bytes as s3dgo_dgen_fill, produced chunk by chunk the way a CPU
+ * ObjectGen::fill_chunk caller sees them (src/data_gen.rs:327-336 over
+ * ObjectGenAlt, src/data_gen_alt.rs:89-149): the current block's PRNG state
+ * and its last drawn word carry over between chunks, so no byte is drawn
+ * twice.  Positions only move forward (a backward position reseeds). */
+typedef struct {
+    uint64_t size, f_num, f_den, seed, U, pos;
+    uint64_t s[4];
+    uint64_t blk;       /* block whose state is in s (UINT64_MAX: none) */
+    uint64_t wnext;     /* index of the next word s yields within the block */
+    uint64_t word;      /* word wnext - 1, as fill_bytes_via_next stores it */
+} s3dgo_dgen_stream;
+
+void s3dgo_dgen_stream_init(s3dgo_dgen_stream *g, uint64_t size, uint64_t dedup, uint64_t f_num,
+                            uint64_t f_den, uint64_t seed) {
+    const uint64_t B = 1ull << 20;
+    g->size = size; g->f_num = f_num; g->f_den = f_den; g->seed = seed; g->pos = 0;
+    g->U = s3dgo_unique_blocks((size + B - 1) / B, dedup == 0 ? 1 : dedup);
+    g->blk = UINT64_MAX; g->wnext = 0; g->word = 0;
+}
+
+/* word wi of the current block (len L): the last partial word follows the
+ * 1..4-byte next_u32 rule of s3dgo_fill_bytes. */
+static inline uint64_t dgen_stream_word(s3dgo_dgen_stream *g, uint64_t wi, uint64_t L) {
+    while (g->wnext <= wi) {
+        uint64_t w = s3dgo_xoshiro_next(g->s);
+        const uint64_t tail = L - 8 * g->wnext;
+        if (tail < 8 && tail <= 4) w >>= 32;
+        g->word = w;
+        ++g->wnext;
+    }
+    return g->word;
+}
+
+uint64_t s3dgo_dgen_stream_fill(s3dgo_dgen_stream *g, uint8_t *dst, uint64_t cap) {
+    const uint64_t B = 1ull << 20;
+    uint64_t n = g->size - g->pos < cap ? g->size - g->pos : cap, done = 0;
+    while (done < n) {
+        const uint64_t i = g->pos / B, off = i * B, L = g->size - off < B ? g->size - off : B;
+        uint64_t o = g->pos - off;
+        if (g->blk != i || g->wnext > o / 8 + 1) {
+            s3dgo_xoshiro_seed(g->s, g->seed ^ ((i % g->U) * 0x9E3779B97F4A7C15ull));
+            g->blk = i; g->wnext = 0;
+        }
+        const uint64_t end = L < o + (n - done) ? L : o + (n - done);
+        uint8_t *d = dst + done;
+        const uint64_t o0 = o;
+        while (o < end && (o & 7)) { *d++ = (uint8_t)(dgen_stream_word(g, o / 8, L) >> (8 * (o & 7))); ++o; }
+        while (o + 8 <= end && 8 * g->wnext == o && o + 8 <= L) {   /* whole words, straight from the PRNG */
+            const uint64_t w = s3dgo_xoshiro_next(g->s);
+            memcpy(d, &w, 8);
+            g->word = w; ++g->wnext; d += 8; o += 8;
+        }
+        while (o < end) { *d++ = (uint8_t)(dgen_stream_word(g, o / 8, L) >> (8 * (o & 7))); ++o; }
+        const uint64_t z = (L * g->f_num) / g->f_den;     /* zero prefix of the block */
+        if (o0 < z) memset(dst + done, 0, (z < end ? z : end) - o0);
+        done += end - o0;
+        g->pos += end - o0;
+    }
+    return n;
+}
+
+/* `threads` threads, each generating objects of obj_size bytes chunk by chunk
+ * into its own chunk-sized buffer until `seconds` have passed; object k of
+ * thread t seeded seed_base + t * 1000003 + k.  Returns the bytes made. */
+typedef struct {
+    uint64_t obj_size, chunk, dedup, f_num, f_den, seed0;
+    double seconds;
+    uint64_t bytes;
+} chunk_bench_job;
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void *chunk_bench_worker(void *arg) {
+    chunk_bench_job *J = (chunk_bench_job *)arg;
+    uint8_t *buf = (uint8_t *)malloc(J->chunk);
+    memset(buf, 1, J->chunk);
+    const double t0 = now_s();
+    for (uint64_t k = 0; now_s() - t0 < J->seconds; ++k) {
+        s3dgo_dgen_stream g;
+        s3dgo_dgen_stream_init(&g, J->obj_size, J->dedup, J->f_num, J->f_den, J->seed0 + k);
+        uint64_t w;
+        while ((w = s3dgo_dgen_stream_fill(&g, buf, J->chunk)) > 0) J->bytes += w;
+    }
+    free(buf);
+    return NULL;
+}
+
+uint64_t s3dgo_dgen_chunk_bench(int threads, uint64_t obj_size, uint64_t chunk, uint64_t dedup, uint64_t f_num,
+                                uint64_t f_den, uint64_t seed_base, double seconds, double *elapsed) {
+    if (threads < 1) threads = 1;
+    chunk_bench_job *J = (chunk_bench_job *)calloc((size_t)threads, sizeof(chunk_bench_job));
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    const double t0 = now_s();
+    int started = 0;
+    for (int t = 0; t < threads; ++t) {
+        J[t] = (chunk_bench_job){obj_size, chunk, dedup, f_num, f_den, seed_base + (uint64_t)t * 1000003ull, seconds, 0};
+        if (pthread_create(&tid[started], NULL, chunk_bench_worker, &J[t]) == 0) ++started;
+    }
+    uint64_t bytes = 0;
+    for (int t = 0; t < started; ++t) {
+        pthread_join(tid[t], NULL);
+        bytes += J[t].bytes;
+    }
+    *elapsed = now_s() - t0;
+    free(J);
+    free(tid);
+    return bytes;
 }

@@ -21,6 +21,9 @@ except Exception:  # pragma: no cover - torch is optional for the product
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("S3DLIO_AMD_LIB") or os.path.join(HERE, "libs3dlio_amd.so")   # override: A/B diagnostics
+if os.environ.get("S3DLIO_AMD_LIB"):   # never silently: the override is named on stderr
+    import sys as _sys
+    print(f"s3dlio_amd: S3DLIO_AMD_LIB override: loading {LIB_PATH}", file=_sys.stderr)
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -142,6 +145,7 @@ SIGNATURES = {
                                        ctypes.POINTER(PutStats)]),
     "s3dg_last_error": (ctypes.c_char_p, []),
     "s3dg_version": (ctypes.c_char_p, []),
+    "s3dg_build_digest": (ctypes.c_char_p, []),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -29,11 +29,42 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 
+DIGEST_MARK = b"S3DG_BUILD_DIGEST="
+
+
+def source_digest() -> str:
+    """Digest of the library sources (every csrc .hip/.cpp/.h/.c, the public
+    header and this build script).  It is compiled into the library
+    (s3dg_build_digest()), so a measurement can prove which sources the timed
+    binary was built from, and staleness is decided by content, not mtime."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(os.listdir(CSRC)):
+        if name.endswith((".hip", ".cpp", ".h", ".c")):
+            with open(os.path.join(CSRC, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    for extra in ("include/s3dlio_gpu.h", "s3dlio_amd/build.py"):
+        with open(os.path.join(ROOT, extra), "rb") as f:
+            h.update(extra.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def embedded_digest(path: str = LIB) -> str | None:
+    """The source digest compiled into a built library (read from the file,
+    without loading it), or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    k = data.find(DIGEST_MARK)
+    if k < 0:
+        return None
+    return data[k + len(DIGEST_MARK):k + len(DIGEST_MARK) + 16].decode("ascii", "replace")
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+    return embedded_digest(LIB) != source_digest()
 
 
 BV_SRC = os.path.join(CSRC, "bytesview.c")
@@ -87,7 +118,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
            # load of every 4 KiB-block workgroup disappears from its critical path
            "-mllvm", "-amdgpu-kernarg-preload-count=16",
            "-I", os.path.join(ROOT, "include"), "-I", CSRC,
-           "-DS3DG_BUILD", "-o", LIB] + SOURCES
+           "-DS3DG_BUILD", f"-DS3DG_BUILD_DIGEST=\"{source_digest()}\"", "-o", LIB] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -291,6 +291,14 @@ extern "C" {
 const char *s3dg_last_error(void) { return g_err.c_str(); }
 const char *s3dg_version(void) { return "s3dlio_amd 0.1.0 (gfx950)"; }
 
+// The source digest this library was built from (build.py compiles it in;
+// the marker lets build.py read it from the file without loading it).
+#ifndef S3DG_BUILD_DIGEST
+#define S3DG_BUILD_DIGEST "unknown-digest00"
+#endif
+static const char kBuildDigestRecord[] __attribute__((used)) = "S3DG_BUILD_DIGEST=" S3DG_BUILD_DIGEST;
+const char *s3dg_build_digest(void) { return kBuildDigestRecord + sizeof("S3DG_BUILD_DIGEST=") - 1; }
+
 uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup) {
     const uint64_t d = dedup == 0 ? 1 : dedup;
     if (d <= 1) return nblocks;
@@ -1203,10 +1211,12 @@ int s3dg_device_free(s3dg_ctx *c, void *p) {
 int s3dg_host_alloc_pinned(uint64_t bytes, void **out) {
     if (!out) return fail(S3DG_EINVAL, "null output");
     HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocDefault), "hipHostMalloc");
+    pinned_register(*out, bytes);   // kernels may store into it directly (s3dg_host.cpp small calls)
     return S3DG_OK;
 }
 
 int s3dg_host_free_pinned(void *p) {
+    pinned_unregister(p);
     HIP_TRY(hipHostFree(p), "hipHostFree");
     return S3DG_OK;
 }

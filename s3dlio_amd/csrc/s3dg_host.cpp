@@ -36,6 +36,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -48,6 +49,15 @@ namespace {
 constexpr uint64_t kChunk = 64ull << 20;       // bytes per device staging chunk
 constexpr uint64_t kSplitMin = 128ull << 20;   // smallest per-slot share of a split call
 constexpr int kMaxSlots = 64;
+// Small calls (<= small_max() bytes) skip the copy engine: the kernel stores
+// straight into pinned host memory (the caller's, when this library allocated
+// it, else a bounce buffer the calling thread copies out of piece by piece
+// while the next pieces are generated).  DESIGN.md §5.8 has the measurements.
+constexpr uint64_t kSmallMaxCap = 16ull << 20;
+constexpr uint64_t kSmallDefault = 4ull << 20;
+constexpr uint64_t kPieceMin = 256ull << 10;   // smallest bounce piece
+constexpr int kPiecesMax = 4;                  // pieces per small call (<= kSmallPieces)
+constexpr int kMaxRings = 64;                  // read-ahead rings in existence at once
 
 #define H_TRY(expr, what)                                                                  \
     do {                                                                                   \
@@ -58,10 +68,11 @@ constexpr int kMaxSlots = 64;
 
 struct Slot {
     int device = 0;
-    std::mutex mu;                      // init and the idle list
+    std::mutex mu;                      // init and the idle lists
     s3dg_ctx *ctx = nullptr;            // set last: non-null = initialised
     void *base_proc[2] = {nullptr, nullptr};   // A_BASE_BLOCK, BASE_BLOCK copies in HBM
     std::vector<HostStaging *> idle;
+    std::vector<HostRing *> rings;      // idle read-ahead rings
 };
 
 struct Pool {
@@ -70,6 +81,7 @@ struct Pool {
     std::vector<Slot *> slots;          // never freed: outlives HIP teardown
     uint8_t proc_base[2][kBlk];         // per-process random blocks (same on every slot)
     std::atomic<uint64_t> ticket{0};
+    std::atomic<int> rings{0};          // read-ahead rings allocated
 };
 
 Pool &pool() {
@@ -156,9 +168,27 @@ void staging_free(HostStaging *sg) {
         if (sg->st[q]) (void)hipStreamDestroy(sg->st[q]);
         if (sg->pin[q]) (void)hipHostFree(sg->pin[q]);
     }
+    if (sg->bounce) {
+        pinned_unregister(sg->bounce);
+        (void)hipHostFree(sg->bounce);
+    }
+    for (auto &e : sg->ev)
+        if (e) (void)hipEventDestroy(e);
     if (sg->base_user) (void)hipFree(sg->base_user);
     delete sg;
 }
+
+uint64_t small_max() {
+    static const uint64_t v = [] {
+        const char *e = getenv("S3DLIO_HOST_SMALL_MAX");   // bytes; 0 = every call through the copy engine
+        if (!e || !*e) return kSmallDefault;
+        const uint64_t x = strtoull(e, nullptr, 10);
+        return x < kSmallMaxCap ? x : kSmallMaxCap;
+    }();
+    return v;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 bool d2h_staged() {
     static const bool staged = [] {
@@ -200,6 +230,50 @@ const void *base_for(Slot *S, HostStaging *sg, const HostJob &J) {
 }  // namespace
 
 namespace s3dg {
+
+namespace {
+struct PinRegistry {
+    std::mutex mu;
+    std::map<uintptr_t, uint64_t> m;   // start -> bytes
+};
+PinRegistry &pinreg() {
+    static PinRegistry *r = new PinRegistry();   // never freed: outlives static teardown
+    return *r;
+}
+}  // namespace
+
+void pinned_register(const void *p, uint64_t n) {
+    if (!p || !n) return;
+    PinRegistry &R = pinreg();
+    std::lock_guard<std::mutex> g(R.mu);
+    R.m[(uintptr_t)p] = n;
+}
+
+void pinned_unregister(const void *p) {
+    PinRegistry &R = pinreg();
+    std::lock_guard<std::mutex> g(R.mu);
+    R.m.erase((uintptr_t)p);
+}
+
+bool pinned_owned(const void *p, uint64_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    PinRegistry &R = pinreg();
+    std::lock_guard<std::mutex> g(R.mu);
+    auto it = R.m.upper_bound(a);
+    if (it == R.m.begin()) return false;
+    --it;
+    return a >= it->first && n <= it->second && a - it->first <= it->second - n;
+}
+
+hipError_t host_alloc_pinned_local(int device, uint64_t bytes, void **out) {
+    *out = nullptr;
+    DeviceScope ds(device);
+    if (!ds.ok()) return ds.err;
+    NumaScope scope(device);
+    const hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) pinned_register(*out, bytes);
+    return e;
+}
 
 int host_slot_count(int *n) {
     Pool &P = pool();
@@ -254,6 +328,54 @@ void host_staging_release(HostStaging *sg) {
     S->idle.push_back(sg);
 }
 
+int host_ring_acquire(int slot, uint64_t half, HostRing **out) {
+    *out = nullptr;
+    Slot *S = nullptr;
+    if (int r = get_slot(slot, &S)) return r;
+    {
+        std::lock_guard<std::mutex> g(S->mu);
+        for (size_t k = 0; k < S->rings.size(); ++k)
+            if (S->rings[k]->half == half) {
+                *out = S->rings[k];
+                S->rings.erase(S->rings.begin() + (long)k);
+                return S3DG_OK;
+            }
+    }
+    Pool &P = pool();
+    if (P.rings.fetch_add(1) >= kMaxRings) {   // enough pinned rings: this generator runs synchronously
+        P.rings.fetch_sub(1);
+        return S3DG_OK;
+    }
+    HostRing *r = new HostRing();
+    r->slot = slot;
+    r->half = half;
+    void *mem = nullptr;
+    hipError_t e = host_alloc_pinned_local(S->device, 2 * half, &mem);
+    DeviceScope ds(S->device);
+    for (int q = 0; q < 2 && e == hipSuccess; ++q) e = hipEventCreateWithFlags(&r->ev[q], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        for (auto &ev : r->ev)
+            if (ev) (void)hipEventDestroy(ev);
+        if (mem) {
+            pinned_unregister(mem);
+            (void)hipHostFree(mem);
+        }
+        delete r;
+        P.rings.fetch_sub(1);
+        return s3dg_internal_fail(S3DG_EHIP, (std::string("read-ahead ring: ") + hipGetErrorString(e)).c_str());
+    }
+    r->mem = (uint8_t *)mem;
+    *out = r;
+    return S3DG_OK;
+}
+
+void host_ring_release(HostRing *r) {
+    if (!r) return;
+    Slot *S = pool().slots[r->slot];
+    std::lock_guard<std::mutex> g(S->mu);
+    S->rings.push_back(r);
+}
+
 // Bytes [pos, pos+n) of the job's object into host `buf` on the staging set's
 // slot: the covering generation blocks go through the two device chunks on
 // two streams (chunk k+1's kernel overlaps chunk k's D2H), then exactly the
@@ -261,9 +383,81 @@ void host_staging_release(HostStaging *sg) {
 // buffers in staged mode, where chunk k's host copy overlaps chunk k+1's
 // kernel and D2H).  On an error the streams are drained before returning, so
 // no copy is still landing in `buf` when the caller sees the failure.
+// The caller's base block into the staging set's device block, unless it is
+// the block uploaded last (a seeded caller passes the same block every call).
+static int upload_user_base(HostStaging *sg, const HostJob &J) {
+    if (J.base != HostJob::kBaseUser) return S3DG_OK;
+    if (sg->base_user_valid && memcmp(sg->base_user_host, J.user_base, kBlk) == 0) return S3DG_OK;
+    sg->base_user_valid = false;
+    H_TRY(hipMemcpy(sg->base_user, J.user_base, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
+    memcpy(sg->base_user_host, J.user_base, kBlk);
+    sg->base_user_valid = true;
+    return S3DG_OK;
+}
+
+int host_launch_blocks(HostStaging *sg, const HostJob &J, uint8_t *dst, uint64_t b_lo, uint64_t b_hi,
+                       hipStream_t st) {
+    Slot *S = pool().slots[sg->slot];
+    if (J.dgen)
+        return s3dg_dgen_fill(S->ctx, dst, J.obj_len, b_lo, b_hi, J.dedup, J.f_num, J.f_den, J.entropy, st);
+    H_TRY(launch_fill_stream(ctx_stream_cfg(S->ctx), dst, J.obj_len, 0, 1, (uint32_t)b_lo, (uint32_t)b_hi,
+                             J.entropy, 0, J.pp, base_for(S, sg, J), st),
+          "launch k_fill_stream(host)");
+    return S3DG_OK;
+}
+
+// A small call without the copy engine.  The kernel writes the covering
+// blocks straight into the caller's buffer when this library allocated it
+// pinned and the blocks end exactly at the request; otherwise into the
+// staging set's pinned bounce buffer in up to kPiecesMax pieces on one
+// stream, and the calling thread copies piece k out while pieces k+1.. are
+// generated.
+static int host_run_small(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
+    if (int r = upload_user_base(sg, J)) return r;
+    const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
+    const uint64_t b0 = pos / unit, b1 = (pos + n + unit - 1) / unit;
+    hipStream_t st = sg->st[0];
+    if (aligned16(buf) && pos % unit == 0 && ((pos + n) % unit == 0 || pos + n == J.obj_len) && pinned_owned(buf, n)) {
+        if (int r = host_launch_blocks(sg, J, buf, b0, b1, st)) return r;
+        H_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
+        return S3DG_OK;
+    }
+    const uint64_t need = small_max() + 2 * kDgenBlock;   // the covering blocks of any small request
+    if (sg->bounce_bytes < need) {
+        if (sg->bounce) {
+            pinned_unregister(sg->bounce);
+            H_TRY(hipHostFree(sg->bounce), "hipHostFree(bounce)");
+            sg->bounce = nullptr;
+            sg->bounce_bytes = 0;
+        }
+        void *p = nullptr;
+        H_TRY(host_alloc_pinned_local(S->device, need, &p), "hipHostMalloc(bounce)");
+        sg->bounce = (uint8_t *)p;
+        sg->bounce_bytes = need;
+    }
+    const uint64_t nb = b1 - b0;
+    const uint64_t min_per = (kPieceMin + unit - 1) / unit;
+    uint64_t per = (nb + kPiecesMax - 1) / kPiecesMax;
+    if (per < min_per) per = min_per;
+    const int np = (int)((nb + per - 1) / per);
+    for (int k = 0; k < np; ++k) {
+        if (!sg->ev[k]) H_TRY(hipEventCreateWithFlags(&sg->ev[k], hipEventDisableTiming), "hipEventCreate");
+        const uint64_t pb = b0 + k * per, pe = pb + per < b1 ? pb + per : b1;
+        if (int r = host_launch_blocks(sg, J, sg->bounce + (pb - b0) * unit, pb, pe, st)) return r;
+        H_TRY(hipEventRecord(sg->ev[k], st), "hipEventRecord");
+    }
+    for (int k = 0; k < np; ++k) {
+        const uint64_t pb = b0 + k * per, pe = pb + per < b1 ? pb + per : b1;
+        H_TRY(hipEventSynchronize(sg->ev[k]), "hipEventSynchronize");
+        const uint64_t lo = pb * unit > pos ? pb * unit : pos;
+        const uint64_t hi = pe * unit < pos + n ? pe * unit : pos + n;
+        if (hi > lo) memcpy(buf + (lo - pos), sg->bounce + (lo - b0 * unit), hi - lo);
+    }
+    return S3DG_OK;
+}
+
 static int host_run_chunks(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
-    if (J.base == HostJob::kBaseUser)
-        H_TRY(hipMemcpy(sg->base_user, J.user_base, kBlk, hipMemcpyHostToDevice), "hipMemcpy(base block)");
+    if (int r = upload_user_base(sg, J)) return r;
     const void *base = base_for(S, sg, J);
     const bool staged = d2h_staged();
     if (staged)
@@ -320,7 +514,8 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     Slot *S = pool().slots[sg->slot];
     DeviceScope ds(S->device);
     H_TRY(ds.err, "hipSetDevice");
-    const int r = host_run_chunks(sg, S, J, buf, pos, n);
+    const int r = n <= small_max() && !d2h_staged() ? host_run_small(sg, S, J, buf, pos, n)
+                                                    : host_run_chunks(sg, S, J, buf, pos, n);
     if (r != S3DG_OK)
         for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);   // nothing lands later
     return r;

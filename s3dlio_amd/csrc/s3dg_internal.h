@@ -163,14 +163,31 @@ LaunchCfg ctx_stream_cfg(const s3dg_ctx *c);   // the context's stream-kernel la
 const void *ctx_base(const s3dg_ctx *c);       // the context's 4 KiB base block in HBM
 
 // ---- host-buffer engine (s3dg_host.cpp) --------------------------------------
+// Pinned host allocations made by this library (s3dg_host_alloc_pinned[_local]
+// and the engine's own bounce buffers and rings): the only host memory a
+// kernel may store into directly.  pinned_owned: [p, p+n) lies inside one.
+void pinned_register(const void *p, uint64_t n);
+void pinned_unregister(const void *p);
+bool pinned_owned(const void *p, uint64_t n);
+// hipHostMalloc from a thread bound to the device's local CPUs (its NUMA node).
+hipError_t host_alloc_pinned_local(int device, uint64_t bytes, void **out);
+
 // Staging set of a host slot: two 64 MiB device chunks, two streams and a
-// 4 KiB device block for a caller's base block.
+// 4 KiB device block for a caller's base block; for small calls a pinned
+// bounce buffer the kernels write straight into (no copy engine) and the
+// events that hand its pieces to the calling thread (lazily).
+constexpr int kSmallPieces = 8;
 struct HostStaging {
     int slot = 0;
     void *buf[2] = {nullptr, nullptr};
     hipStream_t st[2] = {nullptr, nullptr};
     void *base_user = nullptr;
+    uint8_t base_user_host[4096];        // the caller's block last uploaded to base_user
+    bool base_user_valid = false;
     void *pin[2] = {nullptr, nullptr};   // pinned bounce buffers (staged D2H mode only, lazily)
+    uint8_t *bounce = nullptr;           // pinned, small calls (lazily)
+    uint64_t bounce_bytes = 0;
+    hipEvent_t ev[kSmallPieces] = {};
 };
 // What to generate into host memory: the fill_controlled_data / random-data
 // layouts (4 KiB blocks, pp) or DG1 (dgen = true, 1 MiB blocks).
@@ -191,6 +208,25 @@ int host_staging_acquire(int slot, HostStaging **out);
 void host_staging_release(HostStaging *sg);   // waits for its streams
 int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n);
 int host_run_split(HostStaging *sg0, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n);
+// Launch the job's generation blocks [b_lo, b_hi) (4 KiB or, DG1, 1 MiB
+// units) at dst (device or library-pinned host memory) on stream st of the
+// staging set's slot; the caller's base block must already be in place.
+int host_launch_blocks(HostStaging *sg, const HostJob &J, uint8_t *dst, uint64_t b_lo, uint64_t b_hi,
+                       hipStream_t st);
+
+// Read-ahead ring of a streaming generator (s3dg_generator.cpp): 2 halves of
+// `half` bytes of pinned host memory on the slot's NUMA node, written by the
+// keystream kernel directly, one event per half.  Pooled per slot; at most
+// kMaxRings exist at once (host_ring_acquire then returns S3DG_OK with *out
+// null and the generator uses the synchronous path).
+struct HostRing {
+    int slot = 0;
+    uint64_t half = 0;
+    uint8_t *mem = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+int host_ring_acquire(int slot, uint64_t half, HostRing **out);
+void host_ring_release(HostRing *r);   // the caller has waited for its pending halves
 
 // ---- CRC-32 (s3dg_crc.hip) -------------------------------------------------
 uint32_t crc32_host_update(uint32_t crc, const uint8_t *p, uint64_t n);

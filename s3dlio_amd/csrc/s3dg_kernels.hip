@@ -375,7 +375,11 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 // 64*pf blocks ahead (one lane per 128-byte line of records) after their
 // stores, result unused, so they are in that XCD's L2 when its workgroups
 // start.  pf must exceed the resident workgroups / 64.
-template <int NT, int NW, bool ABL = false>
+// FLOOR: the fill with the wall-clock floor compiled in (launches whose
+// rt_floor > 0).  The floor-free instantiation carries none of its code: the
+// conditional real-time read and wait cost launches that never use them
+// 0.3-1 % (round 4 library A/B).
+template <int NT, int NW, bool ABL = false, bool FLOOR = false>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
                                                         uint32_t tshift, const u32x4 *base, uint32_t pace) {
@@ -383,8 +387,8 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     const uint32_t t = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
     // pace: the store-only reference's wave-0 delay (ABL), else the fill's
-    // wall-clock floor before the stores (rt_floor, 0 = none)
-    const uint64_t t0 = (!ABL && pace) ? wall_clock64() : 0;
+    // wall-clock floor before the stores (rt_floor; FLOOR instantiation only)
+    const uint64_t t0 = (!ABL && FLOOR) ? wall_clock64() : 0;
     const uint64_t g = g0 + blockIdx.x;
     const uint64_t tile = g >> tshift;
     // The tile record (64 B) in ONE scalar load, issued first; then the base
@@ -407,7 +411,8 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
         if (wave == 0)
             for (uint32_t q = 0; q < pace; ++q) __builtin_amdgcn_s_sleep(2);
     }
-    gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B, t0, ABL ? 0u : pace);
+    gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B, t0,
+                                 (!ABL && FLOOR) ? pace : 0u);
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
     // 128-byte line (2 records) of the span's records
@@ -911,8 +916,12 @@ void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const u3
 template <int NT, int NW>
 void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
                       uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b, uint32_t rt_floor) {
-    hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b,
-                       rt_floor);
+    if (rt_floor)
+        hipLaunchKernelGGL((k_fill_batch<NT, NW, false, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf,
+                           tshift, b, rt_floor);
+    else
+        hipLaunchKernelGGL((k_fill_batch<NT, NW>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf, tshift, b,
+                           0u);
 }
 
 template <int NT, int NW>

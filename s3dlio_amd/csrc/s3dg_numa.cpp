@@ -95,11 +95,7 @@ extern "C" int s3dg_device_numa_node(int device, int *node) {
 
 extern "C" int s3dg_host_alloc_pinned_local(int device, uint64_t bytes, void **out) {
     if (!out) return s3dg_internal_fail(S3DG_EINVAL, "null output");
-    *out = nullptr;
-    DeviceScope ds(device);
-    if (!ds.ok()) return s3dg_internal_fail(S3DG_EHIP, hipGetErrorString(ds.err));
-    NumaScope scope(device);
-    hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    const hipError_t e = host_alloc_pinned_local(device, bytes, out);
     if (e != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, (std::string("hipHostMalloc: ") + hipGetErrorString(e)).c_str());
     return S3DG_OK;
 }

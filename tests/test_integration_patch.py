@@ -118,3 +118,26 @@ def test_rust_patch_has_dgen_surface():
     for gone in ("pub struct ObjectGen ", "pub struct ObjectGenAlt", "fn begin_object",
                  "pub fn generate_controlled_data_streaming"):
         assert gone not in text, gone
+
+
+def test_pyclass_fields_are_send_and_sync():
+    """pyo3 >= 0.23 rejects a #[pyclass] that is not Sync (assert_pyclass_sync)
+    unless it is marked `unsendable`; the reference pins pyo3 ^0.27
+    (Cargo.toml:99).  A struct of the patch that holds a raw pointer is
+    neither Send nor Sync by itself, so each one a pyclass holds needs both
+    `unsafe impl`s (VERDICT r03 next #1)."""
+    rs, py = read(RS), read(PYO3)
+    raw = {m.group(1) for m in re.finditer(r"pub struct (\w+) \{([^}]*)\}", rs, flags=re.S)
+           if re.search(r"\*(mut|const) ", m.group(2))}
+    assert "DataGenerator" in raw
+    checked = 0
+    for m in re.finditer(r"#\[pyclass\(([^)]*)\)\]\s*(?:pub )?struct (\w+) \{([^}]*)\}", py, flags=re.S):
+        if "unsendable" in m.group(1):
+            continue
+        for ty in re.findall(r"\w+:\s*([A-Za-z_]\w*)", m.group(3)):
+            if ty in raw:
+                checked += 1
+                for tr in ("Send", "Sync"):
+                    assert re.search(rf"unsafe impl {tr} for {ty} \{{\}}", rs), \
+                        f"#[pyclass] {m.group(2)} holds {ty}, which is not {tr}"
+    assert checked >= 1

@@ -10,6 +10,8 @@ import pytest
 from conftest import GOLDEN
 from oracle import oracle_py as P
 
+MiB = 1 << 20
+
 
 def load(name):
     with open(os.path.join(GOLDEN, name)) as f:
@@ -145,3 +147,13 @@ def test_zero_fraction_and_dedup_structure(oracle, golden_base):
     y = oracle.fill_controlled(n, 1, 2, 3, 5, base)
     zf = float((y == 0).mean())
     assert abs(zf - 2 / 3) < 0.01
+
+
+@pytest.mark.parametrize("size,chunk", [(1, 1), (13, 5), (4100, 3), (MiB + 9, 777), (3 * MiB + 5, 65536),
+                                        (2 * MiB + 4, 1 << 20), (5 * MiB + 1, 777777)])
+@pytest.mark.parametrize("d,fn,fd", [(1, 0, 1), (2, 1, 2), (3, 2, 3)])
+def test_dgen_stream_port_equals_dgen_fill(oracle, size, chunk, d, fn, fd):
+    """The CPU streaming port behind bench.py's fill_chunk baselines writes
+    the DG1 bytes whatever the chunk size."""
+    assert bytes(oracle.dgen_stream(size, d, fn, fd, 77 + size, chunk)) == bytes(oracle.dgen_fill(size, d, fn, fd,
+                                                                                                77 + size))

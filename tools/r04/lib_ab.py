@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Library A/B in one process: whole product libraries
+(another commit's sources, or this tree with diagnostic -D flags) loaded side
+by side, each with its own context, and timed on the same workloads with the
+library defaults, interleaved, variant order rotated every round.
+
+    python tools/r04/lib_ab.py --build        # here: builds tools/_build/libab_<name>.so
+    python tools/r04/lib_ab.py                # GPU box: runs LAB_POINTS x variants
+
+Variants (LAB_AB, "name=git-ref|.[:-Dflag ...];..."): git-ref = the sources
+of that commit (git archive), "." = this tree.  Default: r02 final (aa93058),
+r03 final (dedd5d0), this tree, this tree without the batch store floor
+(S3DG_DIAG_NOPACE) and this tree with round 2's 2^22-workgroup grid cap.
+Points: cfg2 / cfg3 / cfg5 (10 000 x 8 MiB streams, d1 c1 / d4 c2 / d2 c3),
+cfg4 (10 000 log-uniform objects, d2 c1.5, batch).  Each sample is LAB_LAUNCHES
+back-to-back launches between two HIP events on one stream.
+Tooling only: nothing in the product imports this."""
+import ctypes, json, os, statistics, subprocess, sys, tarfile, io
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tools", "_build")
+DEFAULT = ("r02=aa93058;r03=dedd5d0;head=.;head_nopace=.:-DS3DG_DIAG_NOPACE=1;"
+           "head_cap22=.:-DS3DG_DIAG_GRID_CAP=4194304")
+SRC_NAMES = ["s3dg_kernels.hip", "s3dg_capi.cpp", "s3dg_jump.cpp", "s3dg_generator.cpp", "s3dg_crc.hip",
+             "s3dg_npz.cpp", "s3dg_object.cpp", "s3dg_put.cpp", "s3dg_numa.cpp", "s3dg_host.cpp", "s3dg_batch.hip"]
+
+
+def variants():
+    out = {}
+    for item in os.environ.get("LAB_AB", DEFAULT).split(";"):
+        name, _, spec = item.partition("=")
+        ref, _, flags = spec.partition(":")
+        out[name.strip()] = (ref.strip(), flags.split())
+    return out
+
+
+def so(name):
+    return os.path.join(OUT, f"libab_{name}.so")
+
+
+def sources(ref):
+    """(include dir, csrc dir) of a git ref's sources, or of this tree."""
+    if ref == ".":
+        return os.path.join(ROOT, "include"), os.path.join(ROOT, "s3dlio_amd", "csrc")
+    dst = os.path.join(OUT, f"src_{ref}")
+    if not os.path.isdir(dst):
+        blob = subprocess.check_output(["git", "-C", ROOT, "archive", ref, "include", "s3dlio_amd/csrc"])
+        with tarfile.open(fileobj=io.BytesIO(blob)) as t:
+            t.extractall(dst)
+    return os.path.join(dst, "include"), os.path.join(dst, "s3dlio_amd", "csrc")
+
+
+def build():
+    os.makedirs(OUT, exist_ok=True)
+    procs = []
+    for name, (ref, flags) in variants().items():
+        inc, csrc = sources(ref)
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-fvisibility=hidden", "-Wno-unused-function", "-mllvm", "-amdgpu-kernarg-preload-count=16",
+               "-I", inc, "-I", csrc, "-DS3DG_BUILD", *flags, "-o", so(name)] + [
+                   os.path.join(csrc, s) for s in SRC_NAMES if os.path.exists(os.path.join(csrc, s))]
+        procs.append(subprocess.Popen(cmd))
+        if len(procs) >= 3:
+            assert procs.pop(0).wait() == 0
+    for p in procs:
+        assert p.wait() == 0
+
+
+def main():
+    if "--build" in sys.argv:
+        build()
+        return
+    import torch
+    from bench import log_uniform_sizes, SEED_BASE
+
+    class ObjDesc(ctypes.Structure):
+        _fields_ = [("dst_off", ctypes.c_uint64), ("size", ctypes.c_uint64), ("entropy", ctypes.c_uint64),
+                    ("dedup", ctypes.c_uint64), ("f_num", ctypes.c_uint32), ("f_den", ctypes.c_uint32)]
+    MiB = 1 << 20
+    n = int(os.environ.get("LAB_N", "10000"))
+    launches = int(os.environ.get("LAB_LAUNCHES", "3"))
+    u64, u32 = ctypes.c_uint64, ctypes.c_uint32
+    libs = {}
+    for name in variants():
+        L = ctypes.CDLL(so(name), mode=os.RTLD_LOCAL)
+        L.s3dg_fill_controlled_stream.argtypes = [ctypes.c_void_p] * 2 + [u64] * 4 + [u32] * 2 + [u64] * 2 + [
+            ctypes.c_void_p]
+        L.s3dg_fill_controlled_batch.argtypes = [ctypes.c_void_p] * 3 + [u64, ctypes.c_void_p]
+        h = ctypes.c_void_p()
+        assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
+        libs[name] = (L, h)
+    sizes = log_uniform_sizes(n)
+    arr = (ObjDesc * n)()
+    off = 0
+    for j, sz in enumerate(sizes):
+        arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), 2, 1, 3)
+        off += (sz + 4095) // 4096 * 4096
+    buf = torch.empty(max(8 * MiB * n, off), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    sh = ctypes.c_void_p(st.cuda_stream)
+    p = ctypes.c_void_p(buf.data_ptr())
+    streams = {"cfg2": (1, 0, 1), "cfg3": (4, 1, 2), "cfg5": (2, 2, 3)}
+    work = {k: 8 * MiB * n for k in streams}
+    work["cfg4"] = sum(sizes)
+
+    def run(L, h, kind):
+        if kind in streams:
+            d, fn, fd = streams[kind]
+            r = L.s3dg_fill_controlled_stream(h, p, 8 * MiB, 8 * MiB, n, d, fn, fd, SEED_BASE, 0, sh)
+        else:
+            r = L.s3dg_fill_controlled_batch(h, p, arr, n, sh)
+        assert r == 0, (kind, r)
+
+    pts = os.environ.get("LAB_POINTS", "cfg2;cfg3;cfg5;cfg4").split(";")
+    names = list(libs)
+    res = {}
+    digests = {}
+    reps = int(os.environ.get("LAB_REPS", "8"))
+    for rep in range(reps):
+        for k in pts:
+            order = names[rep % len(names):] + names[:rep % len(names)]
+            if rep % 2:
+                order.reverse()
+            for name in order:
+                L, h = libs[name]
+                run(L, h, k)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(launches):
+                    run(L, h, k)
+                e1.record(st)
+                torch.cuda.synchronize()
+                res.setdefault((name, k), []).append(launches * work[k] / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+                if rep == 0:   # every variant writes the same bytes
+                    digests.setdefault(k, {})[name] = int(buf[:64 * MiB].to(torch.int64).sum().item())
+        print(f"rep {rep} done", flush=True)
+    for k in pts:
+        same = len(set(digests[k].values())) == 1
+        print(json.dumps({"point": k, "outputs_identical": same}), flush=True)
+        for name in names:
+            v = res[(name, k)]
+            print(json.dumps({"variant": name, "point": k, "GBps_median": round(statistics.median(v), 1),
+                              "min": round(min(v), 1), "max": round(max(v), 1), "n": len(v)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
