@@ -80,9 +80,11 @@ int s3dg_set_store_policy(s3dg_ctx *ctx, int stream_policy, int batch_policy);
  * batch launches separately; 0 = hardware maximum, negative = the default.
  * Defaults, measured on MI355X: 14 (stream); batch launches (and large
  * uniform streams, which run through the batch kernel) per launch: no cap,
- * or 30 when most of the launch's blocks have a zero prefix ending on a 64-B
- * line (64 f_num / f_den whole: compress 2, 4, 8, ...).  A tuning knob; results
- * are identical. */
+ * or 29 resident when most of the launch's blocks have a zero prefix ending on
+ * a 64-B line (64 f_num / f_den whole: compress 2, 4, 8, ...).  A cap of k
+ * reserves the LDS that leaves floor(160 KiB / footprint) resident, which the
+ * 512-B allocation granule can make k - 1 (30 gives 29); s3dg_query_occupancy
+ * reports the resident count.  A tuning knob; results are identical. */
 int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_cu);
 /* Batch kernel (batches and large uniform streams): the stores of each 4 KiB
  * block wait until `ticks` wall-clock ticks (10 ns) after its workgroup
@@ -132,7 +134,9 @@ int s3dg_query_occupancy(s3dg_ctx *ctx, int batch, int *wgs_per_cu);
 uint64_t s3dg_unique_blocks(uint64_t nblocks, uint64_t dedup);
 int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
 /* Launch class of compress (f_num, f_den) for the batch kernel's per-launch
- * settings: 1 = zero prefix ending on a 64-B line (cap 30),
+ * settings: 1 = zero prefix ending on a 64-B line (occupancy
+ * cap: 29 resident workgroups per CU, which s3dg_query_occupancy(ctx, 2, ..)
+ * reports; the 512-B LDS granule admits no footprint giving exactly 30),
  * 2 = zero prefix of at least half the block ending inside a line (store
  * floor 100 ticks), 0 = otherwise, or f_den = 0 (no cap, no floor). */
 int s3dg_zero_class(uint32_t f_num, uint32_t f_den);
@@ -228,7 +232,11 @@ int s3dg_stream_destroy(s3dg_ctx *ctx, void *stream);
 /* Release the context's per-stream launch state (tile maps, batch staging) of
  * `stream`, after draining it: call before destroying a stream the context has
  * launched on, so short-lived streams do not accumulate device memory.
- * s3dg_stream_destroy does this itself.  No-op for an unknown stream. */
+ * s3dg_stream_destroy does this itself.  No-op for an unknown stream.  A
+ * launch on `stream` from another thread may race with the release: it
+ * completes, and the last holder of the state drains the stream and frees it.
+ * s3dg_stream_destroy must not run while another thread still uses `stream`
+ * (the HIP stream itself is destroyed, even when the drain reports an error). */
 int s3dg_stream_release(s3dg_ctx *ctx, void *stream);
 int s3dg_stream_state_count(s3dg_ctx *ctx, uint64_t *n);
 int s3dg_sync(s3dg_ctx *ctx, void *stream);   /* stream NULL: whole device */

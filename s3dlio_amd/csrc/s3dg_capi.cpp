@@ -37,10 +37,13 @@ constexpr int kDefaultOccStream = 14, kDefaultOccBatch = -1;   // batch: -1 = pe
 // Batch-kernel occupancy per launch: uncapped (32
 // resident 1-wave workgroups per CU) unless the launch's zero prefixes end on
 // a 64-B line (compress c with 64 % c == 0: c = 2, 4, 8, ... and ratios such
-// as 4/3), where a cap of 30 (29 resident) writes 3-7 % faster: config 3
+// as 4/3), where a cap of 29 resident workgroups writes 3-7 % faster: config 3
 // 7214-7260 -> 7416-7424 GB/s, d1 c4 6925 -> 7435, d1 c8 6933 -> 7436, while
 // the same cap costs c = 1, 1.5 and 3 (mid-line prefixes) 2-4 %
 // (profiles/r03/diag/cfg3/power/).
+// The target passed to occupancy_lds: asking for 30 gives a 5632-B LDS
+// footprint, i.e. 29 resident (no 512-B granule gives exactly 30), which is
+// what was measured and what s3dg_query_occupancy(ctx, 2, ..) reports.
 constexpr int kOccZeroLines = 30;
 // Zero prefixes of at least half the block that end inside a line (c = 3,
 // 5, 6, 7, ...): uncapped, with the stores held until 100 wall-clock ticks
@@ -123,6 +126,11 @@ struct StreamState {
         hipEvent_t consumed = nullptr;  // device copy may be freed (k_batch_map done; both on `up`)
     } stage[2];
     int next = 0;
+    // lifetime (under the context's mu): users holding the state, and whether
+    // s3dg_stream_release has taken it out of the context's map; the last
+    // holder of a released state drains the stream and frees it
+    int refs = 0;
+    bool dead = false;
 };
 
 struct s3dg_ctx {
@@ -393,14 +401,21 @@ int s3dg_stream_release(s3dg_ctx *c, void *stream) {
         if (it == c->streams.end()) return S3DG_OK;
         S = it->second;
         c->streams.erase(it);
+        S->dead = true;
+        ++S->refs;                               // held by this release until the drain below
     }
     hipError_t e;
     {
-        std::lock_guard<std::mutex> g(S->mu);    // wait for an enqueue in progress; released before S is freed
+        std::lock_guard<std::mutex> g(S->mu);    // wait for an enqueue in progress
         e = hipStreamSynchronize((hipStream_t)stream);
         if (e == hipSuccess && S->up) e = hipStreamSynchronize(S->up);
     }
-    stream_state_free(S);
+    bool last;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        last = --S->refs == 0;
+    }
+    if (last) stream_state_free(S);              // else the last holder drains and frees it (StreamLock)
     HIP_TRY(e, "hipStreamSynchronize(release)");
     return S3DG_OK;
 }
@@ -547,13 +562,45 @@ int s3dg_query_occupancy(s3dg_ctx *c, int batch, int *wgs_per_cu) {
     return S3DG_OK;
 }
 
-// The stream's launch state (created on first use).
-static StreamState *stream_state(s3dg_ctx *c, hipStream_t s) {
-    std::lock_guard<std::mutex> g(c->mu);
-    StreamState *&S = c->streams[s];
-    if (!S) S = new StreamState();
-    return S;
-}
+// The stream's launch state (created on first use), held and locked for the
+// scope: one enqueuing thread per stream at a time, and a concurrent
+// s3dg_stream_release never frees a state someone still holds (ADVICE r03:
+// the holder that drops the last reference of a released state drains the
+// stream and frees it).
+class StreamLock {
+public:
+    StreamLock(s3dg_ctx *c, hipStream_t s) : c_(c), s_(s) {
+        {
+            std::lock_guard<std::mutex> g(c->mu);
+            StreamState *&S = c->streams[s];
+            if (!S) S = new StreamState();
+            S_ = S;
+            ++S_->refs;
+        }
+        S_->mu.lock();
+    }
+    ~StreamLock() {
+        S_->mu.unlock();
+        bool last;
+        {
+            std::lock_guard<std::mutex> g(c_->mu);
+            last = --S_->refs == 0 && S_->dead;
+        }
+        if (last) {
+            (void)hipStreamSynchronize(s_);
+            if (S_->up) (void)hipStreamSynchronize(S_->up);
+            stream_state_free(S_);
+        }
+    }
+    StreamState *get() const { return S_; }
+    StreamLock(const StreamLock &) = delete;
+    StreamLock &operator=(const StreamLock &) = delete;
+
+private:
+    s3dg_ctx *c_;
+    hipStream_t s_;
+    StreamState *S_ = nullptr;
+};
 
 // At least `tiles` records in the stream's map.  Earlier launches on this
 // stream may still read the old map: growing drains the stream first.
@@ -585,8 +632,8 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
             ntiles[sh] = n_objs * ((nb + lead + (1ull << sh) - 1) >> sh);
         const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
         const uint64_t tpo = (nb + lead + (1ull << tshift) - 1) >> tshift;
-        StreamState *S = stream_state(c, s);
-        std::lock_guard<std::mutex> g(S->mu);
+        StreamLock SL(c, s);
+        StreamState *S = SL.get();
         if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
         // the prefix's class from its exact length (pp: 4096 f_num / f_den = floor_len + rem / f_den)
         const int zc = pp.f_den == 0 || (pp.floor_len == 0 && pp.rem == 0) ? kZcNone
@@ -853,8 +900,8 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
     if (!dst_base || !aligned16(dst_base)) return fail(S3DG_EINVAL, "dst_base must be 16-byte aligned");
     hipStream_t s = (hipStream_t)stream;
     const uintptr_t base = (uintptr_t)dst_base;
-    StreamState *S = stream_state(c, s);
-    std::lock_guard<std::mutex> g(S->mu);
+    StreamLock SL(c, s);
+    StreamState *S = SL.get();
     if (!S->up) HIP_TRY(hipStreamCreateWithFlags(&S->up, hipStreamNonBlocking), "hipStreamCreate(upload)");
     for (auto &G : S->stage)
         for (hipEvent_t *ev : {&G.uploaded, &G.consumed})
@@ -1159,8 +1206,8 @@ int s3dg_write_ceiling_tiled(s3dg_ctx *c, void *dst, uint64_t len, uint32_t patt
     if (len == 0) return S3DG_OK;
     hipStream_t s = (hipStream_t)stream;
     const uint64_t nthr = (len / kBlk + 63) / 64;
-    StreamState *S = stream_state(c, s);
-    std::lock_guard<std::mutex> g(S->mu);
+    StreamLock SL(c, s);
+    StreamState *S = SL.get();
     if (int r = tiles_reserve(S, nthr, s)) return r;
     HIP_TRY(launch_write_ceiling(cfg_for(c, true), (uint8_t *)dst, len, pattern, S->tiles, nthr, s),
             "launch k_write_ceiling(tiled)");
@@ -1184,8 +1231,8 @@ int s3dg_write_ceiling_fill(s3dg_ctx *c, void *dst, uint64_t len, uint32_t pace,
     const uint32_t lead = (uint32_t)(((uintptr_t)dst >> 12) & 7);
     const uint32_t tshift = kTileShiftMax;
     const uint64_t tpo = (obj / kBlk + lead + (1ull << tshift) - 1) >> tshift;
-    StreamState *S = stream_state(c, s);
-    std::lock_guard<std::mutex> g(S->mu);
+    StreamLock SL(c, s);
+    StreamState *S = SL.get();
     if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
     LaunchCfg lc = cfg_for(c, true);
     lc.pace = pace;
@@ -1246,8 +1293,11 @@ int s3dg_stream_create(s3dg_ctx *c, void **out) {
 
 int s3dg_stream_destroy(s3dg_ctx *c, void *stream) {
     CTX_SCOPE(c);
-    if (int r = s3dg_stream_release(c, stream)) return r;
-    HIP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+    const int r = s3dg_stream_release(c, stream);
+    std::string first = r ? s3dg_last_error() : "";
+    const hipError_t e = hipStreamDestroy((hipStream_t)stream);   // even when the drain failed
+    if (r) return fail(r, first.c_str());
+    HIP_TRY(e, "hipStreamDestroy");
     return S3DG_OK;
 }
 

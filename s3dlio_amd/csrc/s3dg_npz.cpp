@@ -182,34 +182,45 @@ int s3dg_npz_build(s3dg_ctx *ctx, const uint64_t *shape, int ndim, const char *d
             cap = L.x_data;
         }
         uint32_t cd = 0;
-        if (int r = s3dg_xoshiro_fill(ctx, dev, L.x_data, 2u << 20, 0, s)) return r;   // :376-383
+        // after a failure nothing may still read `dev` or write C->reg when the
+        // next build reuses them: both streams are drained first
+        auto bail = [&](int code, const char *msg) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(C->s_crc);
+            return s3dg_internal_fail(code, msg);
+        };
+        if (int r = s3dg_xoshiro_fill(ctx, dev, L.x_data, 2u << 20, 0, s)) {
+            const std::string m = s3dg_last_error();
+            return bail(r, m.c_str());
+        }   // :376-383
         // The D2H (PCIe) and the CRC kernel (HBM reads) both only read the
         // keystream: the CRC runs on a second stream, hidden under the copy.
         if (hipEventRecord(C->filled, s) != hipSuccess || hipStreamWaitEvent(C->s_crc, C->filled, 0) != hipSuccess)
-            return s3dg_internal_fail(S3DG_EHIP, "npz event");
+            return bail(S3DG_EHIP, "npz event");
         // The CRC kernel is enqueued first on its own stream, then the D2H
         // (which, into pageable memory, returns only when done): the two
         // overlap on the GPU.  The region CRCs are fetched after the D2H, and
         // the < 1 KiB tail is hashed from the host copy, so no two copies are
         // in flight from two host threads.
-        if (crc_tables_device(&C->crc_tab) != hipSuccess) return s3dg_internal_fail(S3DG_EHIP, "crc tables");
+        if (crc_tables_device(&C->crc_tab) != hipSuccess) return bail(S3DG_EHIP, "crc tables");
         const CrcSegPlan P = crc_seg_plan(1, L.x_data, L.x_data);
         if (P.nreg > C->reg_cap) {
+            (void)hipStreamSynchronize(C->s_crc);   // the previous build's CRC may still write it
             if (C->reg) (void)hipFree(C->reg);
             C->reg = nullptr;
             C->reg_cap = 0;
-            if (hipMalloc(&C->reg, P.nreg * 4) != hipSuccess) return s3dg_internal_fail(S3DG_ENOMEM, "hipMalloc(crc)");
+            if (hipMalloc(&C->reg, P.nreg * 4) != hipSuccess) return bail(S3DG_ENOMEM, "hipMalloc(crc)");
             C->reg_cap = P.nreg;
         }
         if (crc_seg_launch(P, (const uint8_t *)dev, C->crc_tab, C->reg, C->s_crc) != hipSuccess)
-            return s3dg_internal_fail(S3DG_EHIP, "launch k_crc32_regions");
+            return bail(S3DG_EHIP, "launch k_crc32_regions");
         if (hipMemcpyAsync(out + L.off_x_data, dev, L.x_data, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
-            return s3dg_internal_fail(S3DG_EHIP, "npz x-data D2H");
+            return bail(S3DG_EHIP, "npz x-data D2H");
         std::vector<uint32_t> regions(P.nreg);
         if (P.nreg && (hipMemcpyAsync(regions.data(), C->reg, P.nreg * 4, hipMemcpyDeviceToHost, C->s_crc) != hipSuccess ||
                        hipStreamSynchronize(C->s_crc) != hipSuccess))
-            return s3dg_internal_fail(S3DG_EHIP, "npz crc regions");
+            return bail(S3DG_EHIP, "npz crc regions");
         const uint8_t *tail = out + L.off_x_data + P.seg_rows * 1024;
         crc_seg_fold(P, regions.data(), &tail, &cd);
         crc_x = crc32_combine(crc_x, cd, L.x_data);                                    // :386

@@ -105,7 +105,10 @@ def _dump_failure(oracle, kind, t, size, d, c, seed, j, got, pay, bad):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,t,n,size,d,c", [
-    ("controlled", "RAW", 70, 3 * MiB + 5, 2, 3),     # 3 chunks of packed objects, ragged size
+    ("controlled", "RAW", 70, 3 * MiB + 5, 2, 3),     # one 256 MiB chunk of packed objects, ragged size
+    # 7 chunks of 64 packed objects: the 4-slot pinned ring wraps (chunk index >= kHostSlots)
+    ("controlled", "RAW", 400, 4 * MiB, 1, 2),
+    ("dgen", "RAW", 1, 1300 * MiB + 3, 2, 2),         # one object in 6 slot-sized pieces (ring wraps)
     ("random", "TFRECORD", 300, 5000, 1, 1),
     ("dgen", "NPZ", 5, 2 * MiB + 17, 2, 2),
     ("controlled", "RAW", 1, 600 * MiB + 123, 1, 1),  # split into 3 slot-sized pieces

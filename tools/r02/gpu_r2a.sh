@@ -2,7 +2,7 @@
 # the lab, the counter list, and PMC passes on the CRC kernel and on the fill
 # vs the store-only shapes.  Every step has its own time limit; the first
 # failure ends the script.
-# usage: bash tools/gpu_r2a.sh <out-subdir>
+# usage: bash tools/r02/gpu_r2a.sh <out-subdir>
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r2a}

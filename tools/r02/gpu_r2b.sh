@@ -1,6 +1,6 @@
 # Round-2 check (tooling): new batch/slot tests, the whole GPU suite, smoke,
 # then the lab on the batch path and the ceilings.
-# usage: bash tools/gpu_r2b.sh <out-subdir>
+# usage: bash tools/r02/gpu_r2b.sh <out-subdir>
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r2b}

@@ -1,7 +1,7 @@
 # Round-2 check (tooling): the binding ABI program, every bench config once
 # (short), the paced store-only ceilings, and EA write-stall counters on the
 # fill vs its ablated form.
-# usage: bash tools/gpu_r2c.sh <out-subdir>
+# usage: bash tools/r02/gpu_r2c.sh <out-subdir>
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r2c}

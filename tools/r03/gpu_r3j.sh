@@ -9,4 +9,4 @@ LAB_VARIANTS="cap26=;cap22=-DS3DG_DIAG_GRID_CAP=4194304" LAB_POINTS="stream2:0:-
 grep '^{' $OUT/grid_cap_ab.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/parity_tests.log 2>&1 || { tail -30 $OUT/parity_tests.log; exit 1; }
 tail -1 $OUT/parity_tests.log
-bash tools/gpu_r3i.sh ${1:-r3j}
+bash tools/r03/gpu_r3i.sh ${1:-r3j}

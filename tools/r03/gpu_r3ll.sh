@@ -1,5 +1,5 @@
 # Round 3: the per-launch batch rule against each alternative on one more box
-# (as tools/gpu_r3y.sh, lab only).  Tooling.
+# (as tools/r03/gpu_r3y.sh, lab only).  Tooling.
 set -o pipefail
 OUT=gpurun_out/${1:-r3ll}
 mkdir -p $OUT

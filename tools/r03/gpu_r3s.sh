@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r3s}
 mkdir -p $OUT
-bash tools/gpu_r3r.sh ${1:-r3s} || exit 1
+bash tools/r03/gpu_r3r.sh ${1:-r3s} || exit 1
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_batch.py -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
 for c in 2 3 4 5; do
