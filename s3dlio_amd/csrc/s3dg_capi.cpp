@@ -993,15 +993,16 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
                 if (H[i].size) H[j++] = H[i];
         }
         const uint64_t recs = tshift == 0 ? span : P.ntiles[tshift];
+        const uint64_t rec_alloc = tshift == 0 ? (recs + 15) & ~15ull : recs;   // dense: dense_rec's groups of 16
         // record map tb: free once the fill two sub-batches back has read it
         const int tb = S->bnext;
         S->bnext ^= 1;
-        if (recs > S->btile_cap[tb]) {
+        if (rec_alloc > S->btile_cap[tb]) {
             HIP_TRY(hipEventSynchronize(S->filled[tb]), "hipEventSynchronize(tile map)");
             if (S->btiles[tb]) (void)hipFree(S->btiles[tb]);
             S->btiles[tb] = nullptr;
             S->btile_cap[tb] = 0;
-            const uint64_t cap = recs < 4096 ? 4096 : recs + recs / 4;
+            const uint64_t cap = rec_alloc < 4096 ? 4096 : rec_alloc + rec_alloc / 4;
             HIP_TRY(hipMalloc(&S->btiles[tb], cap * sizeof(TileRec)), "hipMalloc(tile map)");
             S->btile_cap[tb] = cap;
         }

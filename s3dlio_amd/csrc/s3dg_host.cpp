@@ -34,8 +34,10 @@
 #include <time.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -189,6 +191,78 @@ uint64_t small_max() {
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Copy-out of small calls' bounce pieces.  One thread copies pinned memory
+// the GPU has just written at ~30 GB/s (it is not in any CPU cache), below
+// the ~52 GB/s the kernel writes it over PCIe; so pieces 1.. of a call go to
+// helper threads, each of which waits for its own piece's event, while the
+// calling thread takes piece 0 and any piece no helper has claimed yet.
+// Posting happens right after the launches, so a helper's wake-up overlaps
+// the kernels.  Helpers are shared by all callers; a busy pool only means the
+// caller copies more itself.
+class CopyPool {
+public:
+    struct Job {
+        std::atomic<int> left{0};
+        std::atomic<int> err{0};
+    };
+    struct Task {
+        Job *job;
+        hipEvent_t ev;
+        uint8_t *dst;
+        const uint8_t *src;
+        uint64_t len;
+    };
+    static CopyPool &get() {
+        static CopyPool *p = new CopyPool();   // never freed: its threads outlive static teardown
+        return *p;
+    }
+    void post(const Task *t, int n) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (int k = 0; k < n; ++k) q_.push_back(t[k]);
+        }
+        if (n > 1) cv_.notify_all();
+        else cv_.notify_one();
+    }
+    // A queued task of `job`, if any is still unclaimed.
+    bool take(const Job *job, Task *out) {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto it = q_.begin(); it != q_.end(); ++it)
+            if (it->job == job) {
+                *out = *it;
+                q_.erase(it);
+                return true;
+            }
+        return false;
+    }
+    static void run(const Task &t) {
+        if (hipEventSynchronize(t.ev) != hipSuccess) t.job->err.store(1);
+        else memcpy(t.dst, t.src, t.len);
+        t.job->left.fetch_sub(1, std::memory_order_acq_rel);
+    }
+
+private:
+    static constexpr int kHelpers = kPiecesMax - 1;
+    CopyPool() {
+        for (int k = 0; k < kHelpers; ++k) std::thread([this] { loop(); }).detach();
+    }
+    void loop() {
+        for (;;) {
+            Task t;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return !q_.empty(); });
+                t = q_.front();
+                q_.pop_front();
+            }
+            run(t);
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Task> q_;
+};
 
 bool d2h_staged() {
     static const bool staged = [] {
@@ -446,13 +520,23 @@ static int host_run_small(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *b
         if (int r = host_launch_blocks(sg, J, sg->bounce + (pb - b0) * unit, pb, pe, st)) return r;
         H_TRY(hipEventRecord(sg->ev[k], st), "hipEventRecord");
     }
+    CopyPool::Job job;
+    CopyPool::Task tasks[kSmallPieces];
+    int nt = 0;
     for (int k = 0; k < np; ++k) {
         const uint64_t pb = b0 + k * per, pe = pb + per < b1 ? pb + per : b1;
-        H_TRY(hipEventSynchronize(sg->ev[k]), "hipEventSynchronize");
         const uint64_t lo = pb * unit > pos ? pb * unit : pos;
         const uint64_t hi = pe * unit < pos + n ? pe * unit : pos + n;
-        if (hi > lo) memcpy(buf + (lo - pos), sg->bounce + (lo - b0 * unit), hi - lo);
+        if (hi > lo) tasks[nt++] = {&job, sg->ev[k], buf + (lo - pos), sg->bounce + (lo - b0 * unit), hi - lo};
     }
+    job.left.store(nt, std::memory_order_relaxed);
+    CopyPool &cp = CopyPool::get();
+    if (nt > 1) cp.post(tasks + 1, nt - 1);
+    if (nt > 0) CopyPool::run(tasks[0]);
+    for (CopyPool::Task t; nt > 1 && cp.take(&job, &t);) CopyPool::run(t);
+    for (int spins = 0; job.left.load(std::memory_order_acquire) > 0; ++spins)
+        if (spins > 64) std::this_thread::yield();
+    if (job.err.load()) return s3dg_internal_fail(S3DG_EHIP, "hipEventSynchronize(small call piece)");
     return S3DG_OK;
 }
 

@@ -22,5 +22,5 @@ print(sys.argv[1], d["value"], d["roofline"].get("avg_call_ms"), d["verified_vs_
 PY
 done
 step lib_ab
-LAB_AB="r02=aa93058;r03=dedd5d0;head=." LAB_REPS=8 timeout -k 10 400 python -u tools/r04/lib_ab.py > $OUT/lib_ab.log 2>&1 || exit 1
+LAB_AB="r02=aa93058;r03=dedd5d0;head=.;head_dlin=.:-DS3DG_DIAG_DENSE_LINEAR=1" LAB_POINTS="cfg2;cfg3;cfg5;cfg4;cfg10" LAB_REPS=8 timeout -k 10 500 python -u tools/r04/lib_ab.py > $OUT/lib_ab.log 2>&1 || exit 1
 grep -v "rep " $OUT/lib_ab.log

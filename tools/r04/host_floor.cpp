@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -75,8 +77,33 @@ int main(int argc, char **argv) {
     memset(pin, 1, maxn);
     hipEvent_t ev;
     CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    const size_t sizes[] = {64u << 10, 256u << 10, 1u << 20, 4u << 20, 16u << 20};
-    printf("{\"lab\": \"host_floor\", \"reps\": %d}\n", reps);
+    std::vector<size_t> sizes = {64u << 10, 256u << 10, 1u << 20, 4u << 20, 16u << 20};
+    const bool rev = argc > 2 && strcmp(argv[2], "rev") == 0;   // largest first (a fresh process's first calls)
+    if (rev) std::reverse(sizes.begin(), sizes.end());
+    printf("{\"lab\": \"host_floor\", \"reps\": %d, \"order\": \"%s\"}\n", reps, rev ? "rev" : "fwd");
+    // helper threads for the multi-threaded copy-out variant: spin on a generation counter
+    struct Helper {
+        std::atomic<uint64_t> gen{0}, done{0};
+        hipEvent_t ev = nullptr;
+        uint8_t *dst = nullptr;
+        const uint8_t *src = nullptr;
+        size_t len = 0;
+        std::thread th;
+    };
+    static Helper hp[3];
+    static std::atomic<bool> quit{false};
+    for (auto &h : hp)
+        h.th = std::thread([&h] {
+            uint64_t seen = 0;
+            while (!quit.load()) {
+                const uint64_t g = h.gen.load(std::memory_order_acquire);
+                if (g == seen) continue;
+                seen = g;
+                (void)hipEventSynchronize(h.ev);
+                memcpy(h.dst, h.src, h.len);
+                h.done.store(g, std::memory_order_release);
+            }
+        });
     for (size_t n : sizes) {
         auto fill = [&](void *dst) { CS(s3dg_fill_controlled(ctx, dst, n, 1, 0, 1, 7, s)); };
         std::vector<std::pair<const char *, double>> r;
@@ -164,6 +191,27 @@ int main(int argc, char **argv) {
                              }
                          })});
         }
+        r.push_back({"k2h_pipe4_mt_pageable", median_us(reps, [&] {
+                         const uint64_t nb = n / 4096, per = (nb + 3) / 4;
+                         for (int k = 0; k < 4; ++k) {
+                             const uint64_t b0 = k * per, b1 = std::min<uint64_t>(nb, b0 + per);
+                             CS(s3dg_fill_controlled_range(ctx, (uint8_t *)pin + b0 * 4096, n, b0, b1, 1, 0, 1, 7, s));
+                             CK(hipEventRecord(pe[k], s));
+                             if (k) {
+                                 Helper &h = hp[k - 1];
+                                 h.ev = pe[k];
+                                 h.dst = pg + b0 * 4096;
+                                 h.src = (uint8_t *)pin + b0 * 4096;
+                                 h.len = (b1 - b0) * 4096;
+                                 h.gen.fetch_add(1, std::memory_order_release);
+                             }
+                         }
+                         CK(hipEventSynchronize(pe[0]));
+                         memcpy(pg, pin, std::min<uint64_t>(nb, per) * 4096);
+                         for (auto &h : hp)
+                             while (h.done.load(std::memory_order_acquire) != h.gen.load()) {
+                             }
+                     })});
         if (n >= (1u << 20)) {
             r.push_back({"dgen_dev", median_us(reps, [&] {
                              CS(s3dg_dgen_fill(ctx, dev, n, 0, n >> 20, 1, 0, 1, 9, s));
@@ -179,5 +227,7 @@ int main(int argc, char **argv) {
         printf("}\n");
         fflush(stdout);
     }
+    quit.store(true);
+    for (auto &h : hp) h.th.join();
     return 0;
 }

@@ -9,10 +9,12 @@ library defaults, interleaved, variant order rotated every round.
 
 Variants (LAB_AB, "name=git-ref|.[:-Dflag ...];..."): git-ref = the sources
 of that commit (git archive), "." = this tree.  Default: r02 final (aa93058),
-r03 final (dedd5d0), this tree, this tree without the batch store floor
-(S3DG_DIAG_NOPACE) and this tree with round 2's 2^22-workgroup grid cap.
+r03 final (dedd5d0), this tree (the first session also ran this tree with the
+batch floor compiled out and with round 2's 2^22-workgroup grid cap, flags
+since removed or kept as diagnostics: profiles/r04/lib_ab/).
 Points: cfg2 / cfg3 / cfg5 (10 000 x 8 MiB streams, d1 c1 / d4 c2 / d2 c3),
-cfg4 (10 000 log-uniform objects, d2 c1.5, batch).  Each sample is LAB_LAUNCHES
+cfg4 (10 000 log-uniform objects, d2 c1.5, batch), cfg10 (2 000 000 x
+(20 KiB + 5 B) at a 24 KiB stride, batch, dense layout).  Each sample is LAB_LAUNCHES
 back-to-back launches between two HIP events on one stream.
 Tooling only: nothing in the product imports this."""
 import ctypes, json, os, statistics, subprocess, sys, tarfile, io
@@ -20,8 +22,7 @@ import ctypes, json, os, statistics, subprocess, sys, tarfile, io
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
-DEFAULT = ("r02=aa93058;r03=dedd5d0;head=.;head_nopace=.:-DS3DG_DIAG_NOPACE=1;"
-           "head_cap22=.:-DS3DG_DIAG_GRID_CAP=4194304")
+DEFAULT = "r02=aa93058;r03=dedd5d0;head=."
 SRC_NAMES = ["s3dg_kernels.hip", "s3dg_capi.cpp", "s3dg_jump.cpp", "s3dg_generator.cpp", "s3dg_crc.hip",
              "s3dg_npz.cpp", "s3dg_object.cpp", "s3dg_put.cpp", "s3dg_numa.cpp", "s3dg_host.cpp", "s3dg_batch.hip"]
 
@@ -96,18 +97,26 @@ def main():
     for j, sz in enumerate(sizes):
         arr[j] = ObjDesc(off, sz, SEED_BASE + (j << 32), 2, 1, 3)
         off += (sz + 4095) // 4096 * 4096
-    buf = torch.empty(max(8 * MiB * n, off), dtype=torch.uint8, device="cuda")
+    # config 10's objects: 2 000 000 x (20 KiB + 5 B) at a 24 KiB stride, d1 c1 (dense layout)
+    n10 = int(os.environ.get("LAB_N10", "2000000"))
+    arr10 = (ObjDesc * n10)()
+    for j in range(n10):
+        arr10[j] = ObjDesc(j * 24576, 20 * 1024 + 5, SEED_BASE + (j << 32), 1, 0, 1)
+    buf = torch.empty(max(8 * MiB * n, off, n10 * 24576), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     sh = ctypes.c_void_p(st.cuda_stream)
     p = ctypes.c_void_p(buf.data_ptr())
     streams = {"cfg2": (1, 0, 1), "cfg3": (4, 1, 2), "cfg5": (2, 2, 3)}
     work = {k: 8 * MiB * n for k in streams}
     work["cfg4"] = sum(sizes)
+    work["cfg10"] = n10 * (20 * 1024 + 5)
 
     def run(L, h, kind):
         if kind in streams:
             d, fn, fd = streams[kind]
             r = L.s3dg_fill_controlled_stream(h, p, 8 * MiB, 8 * MiB, n, d, fn, fd, SEED_BASE, 0, sh)
+        elif kind == "cfg10":
+            r = L.s3dg_fill_controlled_batch(h, p, arr10, n10, sh)
         else:
             r = L.s3dg_fill_controlled_batch(h, p, arr, n, sh)
         assert r == 0, (kind, r)
