@@ -102,6 +102,11 @@ int s3dg_set_batch_prefetch(s3dg_ctx *ctx, uint32_t tiles);
  * the objects are 4 KiB-aligned, sorted and non-overlapping); 0 = chosen per
  * sub-batch by cost (default).  Results are identical. */
 int s3dg_set_batch_tile(s3dg_ctx *ctx, uint32_t blocks);
+/* Batch launches with per-launch tile sizes: objects of fewer than `blocks`
+ * 4 KiB blocks go to a launch of their own (each class with the tile size
+ * that suits it), so small objects do not pad large tiles with dead slots;
+ * 0 = one launch, negative = default.  Results are identical. */
+int s3dg_set_batch_split(s3dg_ctx *ctx, int blocks);
 /* 1 = run large uniform streams (>= 64 MiB, objects 32 KiB-aligned relative
  * to each other) through the tiled batch kernel with device-built tile
  * records and the batch launch knobs; 0 = always the 2D stream kernel;

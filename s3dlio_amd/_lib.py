@@ -63,6 +63,7 @@ SIGNATURES = {
     "s3dg_set_batch_prefetch": (c_int, [c_vp, c_u32]),
     "s3dg_set_batch_pace": (c_int, [c_vp, c_int]),
     "s3dg_set_batch_tile": (c_int, [c_vp, c_u32]),
+    "s3dg_set_batch_split": (c_int, [c_vp, c_int]),
     "s3dg_set_stream_tiles": (c_int, [c_vp, c_int]),
     "s3dg_query_occupancy": (c_int, [c_vp, c_int, ctypes.POINTER(c_int)]),
     "s3dg_set_keystream_shape": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_u64, c_int]),

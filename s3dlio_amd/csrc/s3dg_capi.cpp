@@ -18,6 +18,7 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -51,6 +52,12 @@ constexpr int kOccZeroLines = 30;
 // §5.1.2: config 5 7343 -> 7535-7540 GB/s, d1 c3 7115-7181 -> 7407-7450;
 // config 2 would lose 0.4 %, so prefix-free launches keep no floor).
 constexpr int kDefaultBatchRtFloor = -1;   // per launch
+// Mixed-size batches (BASELINE config 4): one tile size per launch leaves the
+// last tile of every object ragged, and small objects (a few blocks in a
+// 64-block tile) are mostly dead slots.  Objects below kDefaultSplitBlocks
+// blocks get a launch of their own, whose tile size is picked for them
+// (DESIGN.md §5.1); 0 = off.
+constexpr uint32_t kDefaultSplitBlocks = 0;
 constexpr uint32_t kRtFloorMidZeros = 100;
 // Launch classes by zero prefix (per launch; batches by majority of blocks)
 enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
@@ -148,6 +155,9 @@ struct s3dg_ctx {
     uint32_t prefetch_tiles = kDefaultPrefetch;   // batch tile-record prefetch distance
     uint32_t tile_shift = 0;           // batch tile = 2^tile_shift blocks; 0 = per launch
     bool tile_force_dense = false;     // batch: one record per 4 KiB granule when the layout allows
+    // batch: objects of fewer blocks go to a launch of their own with their own
+    // tile size (0 = one launch per sub-batch)
+    uint32_t split_blocks = kDefaultSplitBlocks;
     // k_keystream launch shapes, [0] npz keystream, [1] DG1
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
     uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
@@ -516,6 +526,12 @@ int s3dg_set_batch_tile(s3dg_ctx *c, uint32_t blocks) {
     return S3DG_OK;
 }
 
+int s3dg_set_batch_split(s3dg_ctx *c, int blocks) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    c->split_blocks = blocks < 0 ? kDefaultSplitBlocks : (uint32_t)blocks;
+    return S3DG_OK;
+}
+
 int s3dg_set_keystream_shape(s3dg_ctx *c, int mode, int draws, int waves, int wgs_per_cu,
                              uint64_t min_lane_draws, int store_policy) {
     if (!c) return fail(S3DG_EINVAL, "null context");
@@ -838,6 +854,8 @@ private:
 // dense-layout test.
 struct BatchScan {
     uint64_t m = 0, blocks = 0, zc_blocks[3] = {}, ntiles[kTileShiftMax + 1] = {};
+    // objects below the split threshold: count, blocks, tiles per tile size
+    uint64_t ms = 0, blocks_s = 0, ntiles_s[kTileShiftMax + 1] = {};
     uint64_t first_off = 0, last_end = 0;
     bool dense_ok = true;
     int err = S3DG_OK;
@@ -845,10 +863,11 @@ struct BatchScan {
 };
 
 static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P,
-                       s3dg_obj_desc *__restrict out) {
+                       s3dg_obj_desc *__restrict out, uint64_t split) {
     // accumulators in registers (P aliases nothing, but the compiler cannot
     // know that across the staging stores); the checks fold into one flag
     uint64_t m = 0, blocks = 0, zc_blocks[3] = {}, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
+    uint64_t ms = 0, blocks_s = 0, nts[kTileShiftMax + 1] = {};
     bool dense = true, bad = false;
     uint32_t zc_num = 0, zc_den = 1;   // last compress seen and its zero_class
     int zc = kZcNone;
@@ -860,6 +879,11 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
         bad |= (o.dst_off & 15u) != 0 || o.f_den == 0 || o.f_num >= o.f_den || nb >= (1ull << 31);
         const uint64_t x = nb + (((base + o.dst_off) >> 12) & 7);   // blocks behind the XCD lead
         for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) nt[sh] += (x + (1ull << sh) - 1) >> sh;
+        if (nb < split) {
+            ++ms;
+            blocks_s += nb;
+            for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) nts[sh] += (x + (1ull << sh) - 1) >> sh;
+        }
         if (m == 0) first = o.dst_off;
         dense = dense && (m == 0 || o.dst_off >= last) && (o.dst_off & (kBlk - 1)) == 0;
         last = o.dst_off + nb * kBlk;
@@ -885,6 +909,9 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
     }
     P.m = m;
     P.blocks = blocks;
+    P.ms = ms;
+    P.blocks_s = blocks_s;
+    for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles_s[sh] = nts[sh];
     for (int k = 0; k < 3; ++k) P.zc_blocks[k] = zc_blocks[k];
     P.first_off = first;
     P.last_end = last;
@@ -945,7 +972,8 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         uint64_t cut[kPrepParts + 1];
         for (int q = 0; q <= parts; ++q) cut[q] = k0 + (k1 - k0) * (uint64_t)q / (uint64_t)parts;
         BatchScan part[kPrepParts];
-        pool.run(parts, [&](int q) { batch_scan(d, cut[q], cut[q + 1], base, part[q], H + (cut[q] - k0)); });
+        const uint64_t split = c->split_blocks;
+        pool.run(parts, [&](int q) { batch_scan(d, cut[q], cut[q + 1], base, part[q], H + (cut[q] - k0), split); });
         BatchScan P;
         for (int q = 0; q < parts; ++q) {
             const BatchScan &Q = part[q];
@@ -959,6 +987,9 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             P.blocks += Q.blocks;
             for (int k = 0; k < 3; ++k) P.zc_blocks[k] += Q.zc_blocks[k];
             for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles[sh] += Q.ntiles[sh];
+            P.ms += Q.ms;
+            P.blocks_s += Q.blocks_s;
+            for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles_s[sh] += Q.ntiles_s[sh];
         }
         const uint64_t m = P.m;
         if (m == 0) { k0 = k1; continue; }
@@ -992,7 +1023,41 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             for (uint64_t i = 0; i < k1 - k0; ++i)
                 if (H[i].size) H[j++] = H[i];
         }
-        const uint64_t recs = tshift == 0 ? span : P.ntiles[tshift];
+        // two classes (s3dg_set_batch_split): the small objects first, each
+        // class with the tile size the tiled cost model picks for it alone
+        uint64_t ms = 0;
+        uint32_t tsh_s = tshift, tsh_l = tshift;
+        if (tshift && !c->tile_shift && split && P.ms > 0 && P.ms < m) {
+            uint64_t nt_l[kTileShiftMax + 1] = {};
+            for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) nt_l[sh] = P.ntiles[sh] - P.ntiles_s[sh];
+            auto pick = [&](const uint64_t *nt, uint64_t blocks) {
+                uint32_t best_sh = kTileShiftMax;
+                double best = 1e300;
+                for (uint32_t sh = kTileShiftMax; sh >= kTileShiftAutoMin; --sh) {
+                    const double cost = kDeadSlotCostTiled * (double)((nt[sh] << sh) - blocks) +
+                                        kRecordCostTiled * (double)nt[sh];
+                    if (cost < best) { best = cost; best_sh = sh; }
+                }
+                return best_sh;
+            };
+            tsh_s = pick(P.ntiles_s, P.blocks_s);
+            tsh_l = pick(nt_l, P.blocks - P.blocks_s);
+            if (tsh_s != tsh_l) {   // stable partition: small objects first
+                ms = P.ms;
+                std::vector<s3dg_obj_desc> big;
+                big.reserve(m - ms);
+                uint64_t j = 0;
+                for (uint64_t i = 0; i < m; ++i) {
+                    if ((H[i].size + kBlk - 1) / kBlk < split) H[j++] = H[i];
+                    else big.push_back(H[i]);
+                }
+                std::copy(big.begin(), big.end(), H + j);
+            }
+        }
+        const uint64_t recs_s = ms ? P.ntiles_s[tsh_s] : 0;
+        const uint64_t recs = tshift == 0 ? span
+                              : ms      ? recs_s + (P.ntiles[tsh_l] - P.ntiles_s[tsh_l])
+                                        : P.ntiles[tshift];
         const uint64_t rec_alloc = tshift == 0 ? (recs + 15) & ~15ull : recs;   // dense: dense_rec's groups of 16
         // record map tb: free once the fill two sub-batches back has read it
         const int tb = S->bnext;
@@ -1010,13 +1075,27 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         HIP_TRY(hipMemcpyAsync(G.dev, G.host, m * sizeof(s3dg_obj_desc), hipMemcpyHostToDevice, S->up),
                 "hipMemcpyAsync(batch descriptors)");
         HIP_TRY(hipEventRecord(G.uploaded, S->up), "hipEventRecord");
-        if (tshift) {
+        if (ms) {   // the two classes' scans and records, the small class's records first
+            size_t tmp = G.scan_tmp_bytes;
+            HIP_TRY(launch_batch_scan(G.dev, ms, tsh_s, base, G.rec_lo, G.scan_tmp, &tmp, S->up), "hipcub scan");
+            tmp = G.scan_tmp_bytes;
+            HIP_TRY(launch_batch_scan(G.dev + ms, m - ms, tsh_l, base, G.rec_lo + ms, G.scan_tmp, &tmp, S->up),
+                    "hipcub scan");
+        } else if (tshift) {
             size_t tmp = G.scan_tmp_bytes;
             HIP_TRY(launch_batch_scan(G.dev, m, tshift, base, G.rec_lo, G.scan_tmp, &tmp, S->up), "hipcub scan");
         }
         HIP_TRY(hipStreamWaitEvent(S->up, S->filled[tb], 0), "hipStreamWaitEvent");
-        HIP_TRY(launch_batch_map(G.dev, m, G.rec_lo, S->btiles[tb], tshift, base, lead0, P.first_off, S->up),
-                "launch k_batch_map");
+        if (ms) {
+            HIP_TRY(launch_batch_map(G.dev, ms, G.rec_lo, S->btiles[tb], tsh_s, base, lead0, P.first_off, S->up),
+                    "launch k_batch_map");
+            HIP_TRY(launch_batch_map(G.dev + ms, m - ms, G.rec_lo + ms, S->btiles[tb] + recs_s, tsh_l, base, lead0,
+                                     P.first_off, S->up),
+                    "launch k_batch_map");
+        } else {
+            HIP_TRY(launch_batch_map(G.dev, m, G.rec_lo, S->btiles[tb], tshift, base, lead0, P.first_off, S->up),
+                    "launch k_batch_map");
+        }
         HIP_TRY(hipEventRecord(G.consumed, S->up), "hipEventRecord");
         HIP_TRY(hipEventRecord(S->mapped[tb], S->up), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(s, S->mapped[tb], 0), "hipStreamWaitEvent");
@@ -1025,8 +1104,16 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
                                                                    : kZcNone;
         LaunchCfg lcs = cfg_for(c, true, zcls);
         if (tshift == 0) lcs.store = c->store_dense;
-        HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
-                "launch k_fill_batch");
+        if (ms) {
+            HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs_s, tsh_s, S->btiles[tb], c->base_dev, s),
+                    "launch k_fill_batch");
+            HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs - recs_s, tsh_l, S->btiles[tb] + recs_s,
+                                       c->base_dev, s),
+                    "launch k_fill_batch");
+        } else {
+            HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
+                    "launch k_fill_batch");
+        }
         HIP_TRY(hipEventRecord(S->filled[tb], s), "hipEventRecord");
         k0 = k1;
     }

@@ -185,6 +185,11 @@ class Context:
         results are identical."""
         call("s3dg_set_batch_tile", self._h, int(blocks))
 
+    def set_batch_split(self, blocks: int = -1) -> None:
+        """Objects of fewer than `blocks` blocks get a batch launch of their own
+        (0 = one launch, negative = default); results are identical."""
+        call("s3dg_set_batch_split", self._h, int(blocks))
+
     def set_keystream_shape(self, mode: int, draws: int = 0, waves: int = 0, wgs_per_cu: int = 0,
                             min_lane_draws: int = 0, store_policy: int = -1) -> None:
         """k_keystream launch shape for mode 0 (npz keystream) or 1 (DG1);

@@ -48,6 +48,7 @@ def _knobs(ctx, rnd):
     ctx.set_batch_prefetch(rnd.choice([-1, 0, 1, 7, 128, 256, 1 << 20]))
     ctx.set_batch_tile(rnd.choice([0, 0, 1, 2, 4, 8, 16, 32, 64]))
     ctx.set_batch_pace(rnd.choice([-1, -1, 0, 50, 200]))   # wall-clock store floor (per-launch default: -1)
+    ctx.set_batch_split(rnd.choice([-1, -1, 0, 8, 64]))    # small objects' own launch
 
 
 def _reset(ctx):
@@ -57,6 +58,7 @@ def _reset(ctx):
     ctx.set_batch_prefetch(-1)
     ctx.set_batch_tile(0)
     ctx.set_batch_pace(-1)
+    ctx.set_batch_split(-1)
     ctx.set_stream_tiles(-1)
     ctx.set_keystream_shape(0)
     ctx.set_keystream_shape(1)

@@ -8,7 +8,7 @@ mkdir -p $OUT
 step() { echo "== $*" >&2; }
 step tests
 timeout -k 10 600 python -u -m pytest tests/test_gpu_host_small.py tests/test_gpu_datagen.py tests/test_gpu_batch.py \
-    tests/test_capi_binding.py tests/test_objects.py tests/test_npz.py -m gpu -x -q --timeout 300 --timeout-method thread \
+    tests/test_capi_binding.py tests/test_objects.py tests/test_npz.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 300 --timeout-method thread \
     > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -2 $OUT/gpu_tests.log
 step host_floor
@@ -41,5 +41,5 @@ for c in 2 8 9; do
   summ $OUT/bench_cfg$c.log
 done
 step lib_ab
-LAB_AB="r03=dedd5d0;head=.;head_dlin=.:-DS3DG_DIAG_DENSE_LINEAR=1" LAB_POINTS="cfg2;cfg4;cfg10" LAB_REPS=8 timeout -k 10 500 python -u tools/r04/lib_ab.py > $OUT/lib_ab.log 2>&1 || exit 1
+LAB_AB="r03=dedd5d0;head=.;head_dlin=.:-DS3DG_DIAG_DENSE_LINEAR=1;head_lateimg=.:-DS3DG_DIAG_LATEIMG=1" LAB_POINTS="cfg2;cfg4;cfg4@8;cfg4@16;cfg4@64;cfg4@256;cfg10;cfg3" LAB_REPS=8 timeout -k 10 500 python -u tools/r04/lib_ab.py > $OUT/lib_ab.log 2>&1 || exit 1
 grep -v "rep " $OUT/lib_ab.log

@@ -112,6 +112,9 @@ def main():
     work["cfg10"] = n10 * (20 * 1024 + 5)
 
     def run(L, h, kind):
+        kind, _, split = kind.partition("@")      # "cfg4@64": s3dg_set_batch_split(64) for this point
+        if hasattr(L, "s3dg_set_batch_split"):
+            assert L.s3dg_set_batch_split(h, int(split) if split else -1) == 0
         if kind in streams:
             d, fn, fd = streams[kind]
             r = L.s3dg_fill_controlled_stream(h, p, 8 * MiB, 8 * MiB, n, d, fn, fd, SEED_BASE, 0, sh)
@@ -141,7 +144,8 @@ def main():
                     run(L, h, k)
                 e1.record(st)
                 torch.cuda.synchronize()
-                res.setdefault((name, k), []).append(launches * work[k] / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+                res.setdefault((name, k), []).append(launches * work[k.partition("@")[0]] /
+                                                    (e0.elapsed_time(e1) * 1e-3) / 1e9)
                 if rep == 0:   # every variant writes the same bytes
                     digests.setdefault(k, {})[name] = int(buf[:64 * MiB].to(torch.int64).sum().item())
         print(f"rep {rep} done", flush=True)
