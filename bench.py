@@ -561,6 +561,17 @@ def main() -> int:
                     "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": algo_per_launch,
                     "source_digest": src_digest, "library_digest": lib_digest}
+        if kind in ("stream", "batch"):
+            # the zero-class setting the context measured and chose (s3dg_query_zero_tune)
+            zc = lib.s3dg_zero_class(fn, fd)
+            if zc:
+                best, rg, pg, nt = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+                call("s3dg_query_zero_tune", ctx._h, zc, ctypes.byref(best), ctypes.byref(rg), ctypes.byref(pg),
+                     ctypes.byref(nt))
+                roof["zero_tune"] = {"zero_class": zc, "setting": {1: "occupancy cap 29", 2: "store floor 100"}[zc],
+                                     "chosen": "class setting" if best.value == 0 else "plain",
+                                     "class_setting_GBps": round(rg.value, 1), "plain_GBps": round(pg.value, 1),
+                                     "timed_launches": nt.value}
         if ceil:
             roof.update(ceil)
             roof["frac_of_store_only_best"] = round(achieved_gbs / ceil["store_only_best_GBps"], 4)

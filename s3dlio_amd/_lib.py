@@ -71,6 +71,8 @@ SIGNATURES = {
     "s3dg_query_keystream_occupancy": (c_int, [c_vp, c_int, ctypes.POINTER(c_int)]),
     "s3dg_unique_blocks": (c_u64, [c_u64, c_u64]),
     "s3dg_zero_class": (c_int, [c_u32, c_u32]),
+    "s3dg_query_zero_tune": (c_int, [c_vp, c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_u64)]),
     "s3dg_compress_ratio": (c_int, [c_u64, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32)]),
     "s3dg_object_entropy": (c_u64, [c_u64, c_u64]),
     "s3dg_random_data": (c_int, [c_vp, c_vp, c_u64, c_u64, c_vp]),

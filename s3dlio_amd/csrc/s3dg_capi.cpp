@@ -61,6 +61,32 @@ constexpr uint32_t kDefaultSplitBlocks = 0;
 constexpr uint32_t kRtFloorMidZeros = 100;
 // Launch classes by zero prefix (per launch; batches by majority of blocks)
 enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
+// The zero-class settings are checked by measurement (round 4).  The fitted
+// rule (cap for line-aligned prefixes, store floor for mid-line ones) won on
+// some boxes and lost 0.5-1.6 % to a plain launch on others (DESIGN.md
+// §5.1.2): it compensates for the chip's power state, which differs between
+// boxes and over time.  So a context times its own large launches of each zero
+// class (HIP events around the fill, read back without waiting, at a later
+// launch) and runs the rule or the plain uncapped launch, whichever wrote
+// faster, probing the other one again every kTuneReprobe launches.  Launches
+// below kTuneMinBytes use the current choice unmeasured; an explicit
+// s3dg_set_occupancy / s3dg_set_batch_pace (or S3DG_ZC_TUNE=0) turns it off.
+constexpr uint64_t kTuneMinBytes = 1ull << 30;
+constexpr uint64_t kTuneReprobe = 16;
+struct ZcTuner {
+    int best = 0;                  // 0 = the fitted rule, 1 = uncapped, no floor
+    uint64_t launches = 0;         // timed launches issued
+    uint64_t issued[2] = {0, 0};
+    double ema[2] = {0, 0};        // GB/s
+    int samples[2] = {0, 0};
+    struct Pending {
+        hipEvent_t a, b;
+        double bytes;
+        int cand;
+    };
+    std::vector<Pending> pend;
+    std::vector<hipEvent_t> spare;
+};
 constexpr uint32_t kDefaultPrefetch = 256;   // in 64-block units; > resident workgroups / 64
 constexpr int kDefaultStreamTiles = 1;
 constexpr uint64_t kStreamTilesMinBlocks = 16384;   // smaller streams: 2D kernel, no tile-map launch
@@ -172,6 +198,7 @@ struct s3dg_ctx {
     uint32_t *crc_seg = nullptr;       // per-segment CRCs (device)
     uint64_t crc_seg_cap = 0;
     std::mutex crc_mu;
+    ZcTuner tune[3];                   // per zero class (under mu)
     std::mutex mu;
 };
 
@@ -252,6 +279,75 @@ LaunchCfg cfg_for(s3dg_ctx *c, bool batch = false, int zclass = kZcNone) {
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+bool tune_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("S3DG_ZC_TUNE");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+// A launch of class zc writing `bytes`: the candidate to run (0 = the fitted
+// rule, 1 = plain) and whether to time it (*timed, events in *probe).
+int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending *probe) {
+    *timed = false;
+    if (zc == kZcNone || c->occ_batch >= 0 || c->batch_rt_floor >= 0 || !tune_enabled()) return 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    ZcTuner &T = c->tune[zc];
+    // harvest finished measurements (never waits)
+    for (size_t k = 0; k < T.pend.size();) {
+        ZcTuner::Pending &p = T.pend[k];
+        if (hipEventQuery(p.b) != hipSuccess) {
+            (void)hipGetLastError();
+            ++k;
+            continue;
+        }
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess && ms > 0.f) {
+            const double gbs = p.bytes / (ms * 1e6);
+            T.ema[p.cand] = T.samples[p.cand] ? 0.5 * T.ema[p.cand] + 0.5 * gbs : gbs;
+            ++T.samples[p.cand];
+        }
+        (void)hipGetLastError();
+        T.spare.push_back(p.a);
+        T.spare.push_back(p.b);
+        T.pend[k] = T.pend.back();
+        T.pend.pop_back();
+    }
+    if (T.samples[0] && T.samples[1]) T.best = T.ema[1] > T.ema[0] ? 1 : 0;
+    if (bytes < kTuneMinBytes) return T.best;
+    const int cand = !T.issued[0] ? 0 : !T.issued[1] ? 1
+                   : (T.launches % kTuneReprobe == kTuneReprobe - 1) ? 1 - T.best : T.best;
+    if (T.pend.size() < 16) {
+        for (int q = 0; q < 2; ++q) {
+            hipEvent_t &e = q ? probe->b : probe->a;
+            if (!T.spare.empty()) {
+                e = T.spare.back();
+                T.spare.pop_back();
+            } else if (hipEventCreate(&e) != hipSuccess) {
+                (void)hipGetLastError();
+                if (q) T.spare.push_back(probe->a);
+                return cand;
+            }
+        }
+        probe->bytes = (double)bytes;
+        probe->cand = cand;
+        *timed = true;
+    }
+    ++T.launches;
+    ++T.issued[cand];
+    return cand;
+}
+
+// Record the timed launch's events around it (start before, end after).
+void tune_mark(s3dg_ctx *c, int zc, const ZcTuner::Pending &probe, bool end, hipStream_t s) {
+    (void)hipEventRecord(end ? probe.b : probe.a, s);
+    if (end) {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->tune[zc].pend.push_back(probe);
+    }
+}
 
 // Batch tile size: every object's last tile is ragged, and its blocks past
 // the object's end are workgroups that start, load the record and exit.
@@ -394,6 +490,13 @@ int s3dg_ctx_destroy(s3dg_ctx *c) {
     for (auto &kv : c->jtabs) (void)hipFree(kv.second);
     if (c->crc_tab) (void)hipFree(c->crc_tab);
     if (c->crc_seg) (void)hipFree(c->crc_seg);
+    for (auto &T : c->tune) {
+        for (auto &p : T.pend) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : T.spare) (void)hipEventDestroy(e);
+    }
     delete c;
     return S3DG_OK;
 }
@@ -523,6 +626,17 @@ int s3dg_set_batch_tile(s3dg_ctx *c, uint32_t blocks) {
     }
     c->tile_shift = sh;
     c->tile_force_dense = blocks == 1;
+    return S3DG_OK;
+}
+
+int s3dg_query_zero_tune(s3dg_ctx *c, int zclass, int *best, double *rule_gbs, double *plain_gbs, uint64_t *timed) {
+    if (!c || zclass < 0 || zclass > 2) return fail(S3DG_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    const ZcTuner &T = c->tune[zclass];
+    if (best) *best = T.best;
+    if (rule_gbs) *rule_gbs = T.samples[0] ? T.ema[0] : 0.0;
+    if (plain_gbs) *plain_gbs = T.samples[1] ? T.ema[1] : 0.0;
+    if (timed) *timed = T.launches;
     return S3DG_OK;
 }
 
@@ -656,8 +770,15 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
                        : pp.rem == 0 && (pp.floor_len & 63u) == 0      ? kZcLines
                        : 2 * (uint64_t)pp.floor_len >= kBlk            ? kZcMidHeavy
                                                                         : kZcNone;
-        HIP_TRY(launch_fill_uniform_tiles(cfg_for(c, true, zc), dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift,
-                                          lead, seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s),
+        bool timed = false;
+        ZcTuner::Pending probe{};
+        const int cand = tune_pick(c, zc, obj_size * n_objs, &timed, &probe);
+        if (timed) tune_mark(c, zc, probe, false, s);
+        const hipError_t le = launch_fill_uniform_tiles(cfg_for(c, true, cand ? kZcNone : zc), dst, obj_size, stride,
+                                                        n_objs, (uint32_t)tpo, tshift, lead,
+                                                        seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s);
+        if (timed) tune_mark(c, zc, probe, true, s);
+        HIP_TRY(le,
                 "launch k_fill_batch(stream)");
         return S3DG_OK;
     }
@@ -1102,8 +1223,12 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         const int zcls = 2 * P.zc_blocks[kZcLines] > P.blocks      ? kZcLines
                          : 2 * P.zc_blocks[kZcMidHeavy] > P.blocks ? kZcMidHeavy
                                                                    : kZcNone;
-        LaunchCfg lcs = cfg_for(c, true, zcls);
+        bool timed = false;
+        ZcTuner::Pending probe{};
+        const int cand = tune_pick(c, zcls, P.blocks * kBlk, &timed, &probe);
+        LaunchCfg lcs = cfg_for(c, true, cand ? kZcNone : zcls);
         if (tshift == 0) lcs.store = c->store_dense;
+        if (timed) tune_mark(c, zcls, probe, false, s);
         if (ms) {
             HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs_s, tsh_s, S->btiles[tb], c->base_dev, s),
                     "launch k_fill_batch");
@@ -1114,6 +1239,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
                     "launch k_fill_batch");
         }
+        if (timed) tune_mark(c, zcls, probe, true, s);
         HIP_TRY(hipEventRecord(S->filled[tb], s), "hipEventRecord");
         k0 = k1;
     }

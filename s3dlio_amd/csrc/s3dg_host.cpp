@@ -331,12 +331,21 @@ void pinned_unregister(const void *p) {
 
 bool pinned_owned(const void *p, uint64_t n) {
     const uintptr_t a = (uintptr_t)p;
-    PinRegistry &R = pinreg();
-    std::lock_guard<std::mutex> g(R.mu);
-    auto it = R.m.upper_bound(a);
-    if (it == R.m.begin()) return false;
-    --it;
-    return a >= it->first && n <= it->second && a - it->first <= it->second - n;
+    {
+        PinRegistry &R = pinreg();
+        std::lock_guard<std::mutex> g(R.mu);
+        auto it = R.m.upper_bound(a);
+        if (it == R.m.begin()) return false;
+        --it;
+        if (!(a >= it->first && n <= it->second && a - it->first <= it->second - n)) return false;
+    }
+    // and HIP still knows it as pinned host memory (a registry entry outlives a
+    // buffer freed behind the library's back; a kernel must never store into
+    // pageable memory: without XNACK that is a GPU page fault)
+    hipPointerAttribute_t at{};
+    const bool pinned = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return pinned;
 }
 
 hipError_t host_alloc_pinned_local(int device, uint64_t bytes, void **out) {

@@ -24,7 +24,7 @@ print(sys.argv[1], d["value"], d["roofline"].get("avg_call_ms") or d["roofline"]
       d["verified_vs_oracle"], c.get("value"), c.get("min_med_max_GiBps"), c.get("spread"))
 PY
 }
-for c in 18 19 20 23 24 25 27 28; do
+for c in 18 19 20 23 24 26 27; do
   step bench $c
   timeout -k 10 240 python -u bench.py --config $c --steps 3 --warmup 1 --cpu-seconds 5 > $OUT/bench_cfg$c.log 2>&1 || { tail -20 $OUT/bench_cfg$c.log; exit 1; }
   summ $OUT/bench_cfg$c.log
@@ -35,7 +35,7 @@ summ $OUT/bench_cfg18_pinned.log
 step bench 20 small_max=0
 S3DLIO_HOST_SMALL_MAX=0 timeout -k 10 240 python -u bench.py --config 19 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_cfg19_dma.log 2>&1 || exit 1
 summ $OUT/bench_cfg19_dma.log
-for c in 2 8 9; do
+for c in 2 3 5 8 9; do
   step bench $c
   timeout -k 10 300 python -u bench.py --config $c --steps 10 --warmup 2 > $OUT/bench_cfg$c.log 2>&1 || { tail -20 $OUT/bench_cfg$c.log; exit 1; }
   summ $OUT/bench_cfg$c.log
