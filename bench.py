@@ -157,6 +157,8 @@ def parse():
                    help="batch kernel wall-clock store floor in 10-ns ticks (0 = off; default: per launch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-pin", action="store_true",
+                   help="bind the CPU baseline's threads to the cgroup's share of CPUs (GPU-local first)")
     p.add_argument("--no-d2h", action="store_true")
     p.add_argument("--d2h-reps", type=int, default=1, help="D2H-inclusive samples (diagnosis of run-to-run spread)")
     p.add_argument("--d2h-full", action="store_true",
@@ -543,7 +545,7 @@ def main() -> int:
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes, dev=dev)
+        cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes, dev=dev, pin=args.cpu_pin)
 
     if rank == 0:
         if kind == "host":
@@ -934,29 +936,36 @@ def pin_cpus(dev: int, n: int) -> list[int]:
     return (local + [c for c in aff if c not in local])[:n]
 
 
-def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=5):
+def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=5, pin=False):
     """The C restatement of the same generator (oracle, kind 'port') on this
-    host's cores, parallel like the reference's Rayon loops: `reps` samples of
-    seconds/reps each, the median reported with min and max (VERDICT r03
-    next #5), its threads pinned to the cgroup's share of CPUs (those on the
-    GPU's NUMA node first; threads inherit the calling thread's affinity)."""
+    host's cores, parallel like the reference's Rayon loops: a warm-up sample,
+    then `reps` samples of seconds/reps each, the median reported with min and
+    max.  pin: threads bound to the cgroup's share of
+    CPUs, those on the GPU's NUMA node first (threads inherit the calling
+    thread's affinity); off by default: on the shared 256-CPU host a pinned
+    set shares its CPUs with other jobs' threads, and the samples spread
+    10-400 % (profiles/r04/bench/d_*), where the scheduler left free to
+    migrate keeps them within a few per cent."""
     share = cpu_share()
-    cpus = pin_cpus(dev, share["threads"])
+    cpus = pin_cpus(dev, share["threads"]) if pin else None
     saved = os.sched_getaffinity(0)
     runs = []
     try:
-        os.sched_setaffinity(0, cpus)
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+        _cpu_sample(cfg, fn, fd, min(1.0, seconds / reps), sizes, share)   # warm-up: pools, rings, pages
         for _ in range(reps):
             runs.append(_cpu_sample(cfg, fn, fd, seconds / reps, sizes, share))
     finally:
-        os.sched_setaffinity(0, saved)
+        if cpus:
+            os.sched_setaffinity(0, saved)
     vals = sorted(r["value"] for r in runs)
     med = vals[len(vals) // 2]
     out = dict(next(r for r in runs if r["value"] == med))
     out.update(value=med, samples_GiBps=[r["value"] for r in runs],
                min_med_max_GiBps=[vals[0], med, vals[-1]],
                spread=round((vals[-1] - vals[0]) / med, 4) if med else None,
-               pinned_cpus=f"{len(cpus)} CPUs: {cpus[0]}-{cpus[-1]}" if cpus else None,
+               pinned_cpus=f"{len(cpus)} CPUs: {cpus[0]}-{cpus[-1]}" if cpus else "no (scheduler's choice)",
                sample=f"median of {reps} samples; one sample: " + out["sample"])
     return out
 

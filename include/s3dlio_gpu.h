@@ -145,13 +145,15 @@ int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
  * 2 = zero prefix of at least half the block ending inside a line (store
  * floor 100 ticks), 0 = otherwise, or f_den = 0 (no cap, no floor). */
 int s3dg_zero_class(uint32_t f_num, uint32_t f_den);
-/* Batch-kernel launches of zero class 1 or 2 (above) check their settings by
+/* Batch-kernel launches of zero class 2 (above) check their store floor by
  * measurement: the context times its own launches of >= 1 GiB and runs the
- * class's setting (cap or floor) or a plain launch, whichever wrote faster,
- * re-probing the other now and then; an explicit s3dg_set_occupancy /
- * s3dg_set_batch_pace (or env S3DG_ZC_TUNE=0) turns this off.  Query: the
- * choice (0 = the class setting, 1 = plain), each one's recent GB/s (0 =
- * not measured yet) and the timed launch count.  Results are identical. */
+ * floor or a plain launch, whichever wrote faster (best of each one's last
+ * three rates, after two launches of each), re-probing the other every 16
+ * launches; class 1 keeps its cap.  An explicit s3dg_set_occupancy /
+ * s3dg_set_batch_pace (or env S3DG_ZC_TUNE=0) turns this off.  Query (zclass
+ * 0-2): the choice (0 = the class setting, 1 = plain), each one's best recent
+ * GB/s (0 = not measured yet) and the timed launch count.  Results are
+ * identical. */
 int s3dg_query_zero_tune(s3dg_ctx *ctx, int zclass, int *best, double *rule_gbs, double *plain_gbs,
                          uint64_t *timed);
 /* Per-object entropy of object j of a stream: seed_base + j * 2^32. */

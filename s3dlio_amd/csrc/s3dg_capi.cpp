@@ -61,23 +61,26 @@ constexpr uint32_t kDefaultSplitBlocks = 0;
 constexpr uint32_t kRtFloorMidZeros = 100;
 // Launch classes by zero prefix (per launch; batches by majority of blocks)
 enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
-// The zero-class settings are checked by measurement (round 4).  The fitted
-// rule (cap for line-aligned prefixes, store floor for mid-line ones) won on
-// some boxes and lost 0.5-1.6 % to a plain launch on others (DESIGN.md
-// §5.1.2): it compensates for the chip's power state, which differs between
-// boxes and over time.  So a context times its own large launches of each zero
+// The mid-line class's store floor is checked by measurement (round 4).  It
+// won 2.6 % on one box and lost 0.5-1.6 % to a plain launch on four others
+// (DESIGN.md §5.1.2): it compensates for the chip's power state, which
+// differs between boxes.  So a context times its own large launches of that
 // class (HIP events around the fill, read back without waiting, at a later
-// launch) and runs the rule or the plain uncapped launch, whichever wrote
-// faster, probing the other one again every kTuneReprobe launches.  Launches
-// below kTuneMinBytes use the current choice unmeasured; an explicit
-// s3dg_set_occupancy / s3dg_set_batch_pace (or S3DG_ZC_TUNE=0) turns it off.
+// launch) and runs the floor or the plain uncapped launch, whichever wrote
+// faster: the best of each one's last kTuneKeep rates, after kTuneFirst
+// launches of each (a process's first launch is slow), probing the loser
+// again every kTuneReprobe launches.  The line-aligned class keeps its cap
+// unmeasured: it won 4-9 % on every box.  Launches below kTuneMinBytes use
+// the current choice; an explicit s3dg_set_occupancy / s3dg_set_batch_pace
+// (or S3DG_ZC_TUNE=0) turns the check off.
 constexpr uint64_t kTuneMinBytes = 1ull << 30;
 constexpr uint64_t kTuneReprobe = 16;
+constexpr int kTuneKeep = 3, kTuneFirst = 2;
 struct ZcTuner {
     int best = 0;                  // 0 = the fitted rule, 1 = uncapped, no floor
     uint64_t launches = 0;         // timed launches issued
     uint64_t issued[2] = {0, 0};
-    double ema[2] = {0, 0};        // GB/s
+    double recent[2][kTuneKeep] = {};   // GB/s of the last kTuneKeep timed launches of each
     int samples[2] = {0, 0};
     struct Pending {
         hipEvent_t a, b;
@@ -292,7 +295,7 @@ bool tune_enabled() {
 // rule, 1 = plain) and whether to time it (*timed, events in *probe).
 int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending *probe) {
     *timed = false;
-    if (zc == kZcNone || c->occ_batch >= 0 || c->batch_rt_floor >= 0 || !tune_enabled()) return 0;
+    if (zc != kZcMidHeavy || c->occ_batch >= 0 || c->batch_rt_floor >= 0 || !tune_enabled()) return 0;
     std::lock_guard<std::mutex> g(c->mu);
     ZcTuner &T = c->tune[zc];
     // harvest finished measurements (never waits)
@@ -305,8 +308,7 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
         }
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess && ms > 0.f) {
-            const double gbs = p.bytes / (ms * 1e6);
-            T.ema[p.cand] = T.samples[p.cand] ? 0.5 * T.ema[p.cand] + 0.5 * gbs : gbs;
+            T.recent[p.cand][T.samples[p.cand] % kTuneKeep] = p.bytes / (ms * 1e6);
             ++T.samples[p.cand];
         }
         (void)hipGetLastError();
@@ -315,10 +317,16 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
         T.pend[k] = T.pend.back();
         T.pend.pop_back();
     }
-    if (T.samples[0] && T.samples[1]) T.best = T.ema[1] > T.ema[0] ? 1 : 0;
+    if (T.samples[0] >= kTuneFirst && T.samples[1] >= kTuneFirst) {
+        double top[2] = {0, 0};
+        for (int q = 0; q < 2; ++q)
+            for (int k = 0; k < kTuneKeep && k < T.samples[q]; ++k) top[q] = std::max(top[q], T.recent[q][k]);
+        T.best = top[1] > top[0] ? 1 : 0;
+    }
     if (bytes < kTuneMinBytes) return T.best;
-    const int cand = !T.issued[0] ? 0 : !T.issued[1] ? 1
-                   : (T.launches % kTuneReprobe == kTuneReprobe - 1) ? 1 - T.best : T.best;
+    const int cand = T.issued[0] < (uint64_t)kTuneFirst || T.issued[1] < (uint64_t)kTuneFirst
+                         ? (int)(T.launches & 1)                                 // rule, plain, rule, plain
+                     : (T.launches % kTuneReprobe == kTuneReprobe - 1) ? 1 - T.best : T.best;
     if (T.pend.size() < 16) {
         for (int q = 0; q < 2; ++q) {
             hipEvent_t &e = q ? probe->b : probe->a;
@@ -633,9 +641,12 @@ int s3dg_query_zero_tune(s3dg_ctx *c, int zclass, int *best, double *rule_gbs, d
     if (!c || zclass < 0 || zclass > 2) return fail(S3DG_EINVAL, "bad argument");
     std::lock_guard<std::mutex> g(c->mu);
     const ZcTuner &T = c->tune[zclass];
+    double top[2] = {0, 0};
+    for (int q = 0; q < 2; ++q)
+        for (int k = 0; k < kTuneKeep && k < T.samples[q]; ++k) top[q] = std::max(top[q], T.recent[q][k]);
     if (best) *best = T.best;
-    if (rule_gbs) *rule_gbs = T.samples[0] ? T.ema[0] : 0.0;
-    if (plain_gbs) *plain_gbs = T.samples[1] ? T.ema[1] : 0.0;
+    if (rule_gbs) *rule_gbs = top[0];
+    if (plain_gbs) *plain_gbs = top[1];
     if (timed) *timed = T.launches;
     return S3DG_OK;
 }
@@ -1179,7 +1190,7 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         const uint64_t recs = tshift == 0 ? span
                               : ms      ? recs_s + (P.ntiles[tsh_l] - P.ntiles_s[tsh_l])
                                         : P.ntiles[tshift];
-        const uint64_t rec_alloc = tshift == 0 ? (recs + 15) & ~15ull : recs;   // dense: dense_rec's groups of 16
+        const uint64_t rec_alloc = recs;
         // record map tb: free once the fill two sub-batches back has read it
         const int tb = S->bnext;
         S->bnext ^= 1;

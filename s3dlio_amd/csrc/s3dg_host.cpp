@@ -34,10 +34,8 @@
 #include <time.h>
 
 #include <atomic>
-#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -51,12 +49,19 @@ namespace {
 constexpr uint64_t kChunk = 64ull << 20;       // bytes per device staging chunk
 constexpr uint64_t kSplitMin = 128ull << 20;   // smallest per-slot share of a split call
 constexpr int kMaxSlots = 64;
-// Small calls (<= small_max() bytes) skip the copy engine: the kernel stores
-// straight into pinned host memory (the caller's, when this library allocated
-// it, else a bounce buffer the calling thread copies out of piece by piece
-// while the next pieces are generated).  DESIGN.md §5.8 has the measurements.
+// Calls that skip the copy engine (DESIGN.md §5.8 has the measurements):
+// * into pinned memory this library allocated, up to kDirectMax bytes: the
+//   kernel stores the caller's bytes straight into it (1 MiB 33 us against
+//   42 us through the copy engine; 4 MiB 94 against 103);
+// * into any other buffer, up to small_max() bytes: the kernel stores into a
+//   pinned bounce buffer in pieces, and the calling thread copies piece k out
+//   while pieces k+1.. are generated (64 KiB 16 us against 26, 1 MiB 55
+//   against 76).  Above ~1 MiB one thread's copy out of memory the GPU has
+//   just written (~30 GB/s) loses to HIP's own pageable copy path, and
+//   helper threads for the copy-out measured no faster.
 constexpr uint64_t kSmallMaxCap = 16ull << 20;
-constexpr uint64_t kSmallDefault = 4ull << 20;
+constexpr uint64_t kDirectMax = 16ull << 20;
+constexpr uint64_t kSmallDefault = 1ull << 20;
 constexpr uint64_t kPieceMin = 256ull << 10;   // smallest bounce piece
 constexpr int kPiecesMax = 4;                  // pieces per small call (<= kSmallPieces)
 constexpr int kMaxRings = 64;                  // read-ahead rings in existence at once
@@ -191,78 +196,6 @@ uint64_t small_max() {
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
-
-// Copy-out of small calls' bounce pieces.  One thread copies pinned memory
-// the GPU has just written at ~30 GB/s (it is not in any CPU cache), below
-// the ~52 GB/s the kernel writes it over PCIe; so pieces 1.. of a call go to
-// helper threads, each of which waits for its own piece's event, while the
-// calling thread takes piece 0 and any piece no helper has claimed yet.
-// Posting happens right after the launches, so a helper's wake-up overlaps
-// the kernels.  Helpers are shared by all callers; a busy pool only means the
-// caller copies more itself.
-class CopyPool {
-public:
-    struct Job {
-        std::atomic<int> left{0};
-        std::atomic<int> err{0};
-    };
-    struct Task {
-        Job *job;
-        hipEvent_t ev;
-        uint8_t *dst;
-        const uint8_t *src;
-        uint64_t len;
-    };
-    static CopyPool &get() {
-        static CopyPool *p = new CopyPool();   // never freed: its threads outlive static teardown
-        return *p;
-    }
-    void post(const Task *t, int n) {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            for (int k = 0; k < n; ++k) q_.push_back(t[k]);
-        }
-        if (n > 1) cv_.notify_all();
-        else cv_.notify_one();
-    }
-    // A queued task of `job`, if any is still unclaimed.
-    bool take(const Job *job, Task *out) {
-        std::lock_guard<std::mutex> g(mu_);
-        for (auto it = q_.begin(); it != q_.end(); ++it)
-            if (it->job == job) {
-                *out = *it;
-                q_.erase(it);
-                return true;
-            }
-        return false;
-    }
-    static void run(const Task &t) {
-        if (hipEventSynchronize(t.ev) != hipSuccess) t.job->err.store(1);
-        else memcpy(t.dst, t.src, t.len);
-        t.job->left.fetch_sub(1, std::memory_order_acq_rel);
-    }
-
-private:
-    static constexpr int kHelpers = kPiecesMax - 1;
-    CopyPool() {
-        for (int k = 0; k < kHelpers; ++k) std::thread([this] { loop(); }).detach();
-    }
-    void loop() {
-        for (;;) {
-            Task t;
-            {
-                std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [this] { return !q_.empty(); });
-                t = q_.front();
-                q_.pop_front();
-            }
-            run(t);
-        }
-    }
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Task> q_;
-};
 
 bool d2h_staged() {
     static const bool staged = [] {
@@ -489,18 +422,26 @@ int host_launch_blocks(HostStaging *sg, const HostJob &J, uint8_t *dst, uint64_t
     return S3DG_OK;
 }
 
-// A small call without the copy engine.  The kernel writes the covering
-// blocks straight into the caller's buffer when this library allocated it
-// pinned and the blocks end exactly at the request; otherwise into the
-// staging set's pinned bounce buffer in up to kPiecesMax pieces on one
-// stream, and the calling thread copies piece k out while pieces k+1.. are
-// generated.
-static int host_run_small(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n) {
+// The kernel may write the request's covering blocks straight into `buf`:
+// pinned memory this library allocated, 16-B aligned, and the blocks start
+// and end exactly at the request.
+static bool direct_target(const HostJob &J, const uint8_t *buf, uint64_t pos, uint64_t n) {
+    const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
+    return n <= kDirectMax && aligned16(buf) && pos % unit == 0 && ((pos + n) % unit == 0 || pos + n == J.obj_len) &&
+           pinned_owned(buf, n);
+}
+
+// A call without the copy engine: straight into the caller's buffer
+// (direct_target), or through the staging set's pinned bounce buffer in up
+// to kPiecesMax pieces on one stream, the calling thread copying piece k out
+// while pieces k+1.. are generated.
+static int host_run_small(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n,
+                          bool direct) {
     if (int r = upload_user_base(sg, J)) return r;
     const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
     const uint64_t b0 = pos / unit, b1 = (pos + n + unit - 1) / unit;
     hipStream_t st = sg->st[0];
-    if (aligned16(buf) && pos % unit == 0 && ((pos + n) % unit == 0 || pos + n == J.obj_len) && pinned_owned(buf, n)) {
+    if (direct) {
         if (int r = host_launch_blocks(sg, J, buf, b0, b1, st)) return r;
         H_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
         return S3DG_OK;
@@ -529,23 +470,13 @@ static int host_run_small(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *b
         if (int r = host_launch_blocks(sg, J, sg->bounce + (pb - b0) * unit, pb, pe, st)) return r;
         H_TRY(hipEventRecord(sg->ev[k], st), "hipEventRecord");
     }
-    CopyPool::Job job;
-    CopyPool::Task tasks[kSmallPieces];
-    int nt = 0;
     for (int k = 0; k < np; ++k) {
         const uint64_t pb = b0 + k * per, pe = pb + per < b1 ? pb + per : b1;
+        H_TRY(hipEventSynchronize(sg->ev[k]), "hipEventSynchronize");
         const uint64_t lo = pb * unit > pos ? pb * unit : pos;
         const uint64_t hi = pe * unit < pos + n ? pe * unit : pos + n;
-        if (hi > lo) tasks[nt++] = {&job, sg->ev[k], buf + (lo - pos), sg->bounce + (lo - b0 * unit), hi - lo};
+        if (hi > lo) memcpy(buf + (lo - pos), sg->bounce + (lo - b0 * unit), hi - lo);
     }
-    job.left.store(nt, std::memory_order_relaxed);
-    CopyPool &cp = CopyPool::get();
-    if (nt > 1) cp.post(tasks + 1, nt - 1);
-    if (nt > 0) CopyPool::run(tasks[0]);
-    for (CopyPool::Task t; nt > 1 && cp.take(&job, &t);) CopyPool::run(t);
-    for (int spins = 0; job.left.load(std::memory_order_acquire) > 0; ++spins)
-        if (spins > 64) std::this_thread::yield();
-    if (job.err.load()) return s3dg_internal_fail(S3DG_EHIP, "hipEventSynchronize(small call piece)");
     return S3DG_OK;
 }
 
@@ -607,8 +538,9 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     Slot *S = pool().slots[sg->slot];
     DeviceScope ds(S->device);
     H_TRY(ds.err, "hipSetDevice");
-    const int r = n <= small_max() && !d2h_staged() ? host_run_small(sg, S, J, buf, pos, n)
-                                                    : host_run_chunks(sg, S, J, buf, pos, n);
+    const bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
+    const int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct)
+                                                                : host_run_chunks(sg, S, J, buf, pos, n);
     if (r != S3DG_OK)
         for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);   // nothing lands later
     return r;

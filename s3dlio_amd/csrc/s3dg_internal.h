@@ -62,23 +62,6 @@ struct TileRec {
 };
 static_assert(sizeof(TileRec) == 64, "TileRec is one s_load_dwordx16");
 
-// Dense layout (one record per 4 KiB slot): record of slot q.  Slots are
-// dealt round-robin to the 8 XCDs (slot q on XCD q mod 8), so in slot order
-// a 128-B line holds the records of two XCDs and each XCD's L2 fetches every
-// line; interleaved in groups of 16 slots, a line holds slots q and q + 8,
-// both of one XCD, and each record line is fetched once (round 4: config 10's
-// FETCH_SIZE was twice its record bytes).  The map needs round16(slots)
-// records.  S3DG_DIAG_DENSE_LINEAR=1 (diagnostic builds) keeps slot order.
-#ifndef S3DG_DIAG_DENSE_LINEAR
-#define S3DG_DIAG_DENSE_LINEAR 0
-#endif
-__host__ __device__ inline uint64_t dense_rec(uint64_t q) {
-#if S3DG_DIAG_DENSE_LINEAR
-    return q;
-#else
-    return (q & ~15ull) | ((q & 7) << 1) | ((q >> 3) & 1);
-#endif
-}
 
 // store cache policy of the fill kernels (s3dg_set_store_policy)
 constexpr int kStorePlain = 0, kStoreNT = 1, kStoreSC1 = 2, kStoreNTSC1 = 3;

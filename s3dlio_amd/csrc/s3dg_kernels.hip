@@ -382,11 +382,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 #ifndef S3DG_DIAG_LATEIMG
 #define S3DG_DIAG_LATEIMG 0
 #endif
-// DENSE: the dense layout's instantiation (tshift 0, records interleaved by
-// dense_rec); the tiled instantiations carry none of its index arithmetic,
-// which sits on the path to the record load (a select there cost the tiled
-// launches 0.4-0.9 %, round 4 library A/B).
-template <int NT, int NW, bool ABL = false, bool FLOOR = false, bool DENSE = false>
+template <int NT, int NW, bool ABL = false, bool FLOOR = false>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
                                                         uint32_t tshift, const u32x4 *base, uint32_t pace) {
@@ -397,7 +393,7 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     // wall-clock floor before the stores (rt_floor; FLOOR instantiation only)
     const uint64_t t0 = (!ABL && FLOOR) ? wall_clock64() : 0;
     const uint64_t g = g0 + blockIdx.x;
-    const uint64_t tile = DENSE ? dense_rec(g) : g >> tshift;
+    const uint64_t tile = g >> tshift;
     // The tile record (64 B) in ONE scalar load, issued first; then the base
     // block's vector loads and its LDS image, so the two memory latencies
     // overlap instead of following each other (the compiler otherwise splits
@@ -434,15 +430,13 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     const uint32_t span = kPfSpan > (2u << tshift) ? kPfSpan : (2u << tshift);
     if (pf && (g & (span - 1)) < 8) {
         const uint64_t first = ((g + 64ull * pf) & ~(uint64_t)(span - 1)) >> tshift;
-        if constexpr (DENSE) {
+        if (tshift == 0) {
             // one record per block: this workgroup's XCD (g mod 8, dealt
             // round-robin) uses only the records = g (mod 8) of the span, so
             // it touches those 32 and leaves the rest to the other XCDs
-            // (interleaved map, dense_rec: slots first + 8t + x and + 8(t+1) + x
-            // share a line, so the even t cover the XCD's lines)
-            if (t < span / 8 && !(t & 1)) {
+            if (t < span / 8) {
                 const uint64_t pt = first + 8 * t + (g & 7);
-                const TileRec *p = tiles + dense_rec(pt < ntiles ? pt : ntiles - 1);
+                const TileRec *p = tiles + (pt < ntiles ? pt : ntiles - 1);
                 uint32_t dummy;
                 asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(p) : "memory");
             }
@@ -518,7 +512,7 @@ __global__ __launch_bounds__(256) void k_batch_map(const s3dg_obj_desc *d, uint6
     if (own)
         for (uint64_t q = rec_lo; q < rec_hi; ++q) {
             r.first = (uint32_t)((q - rec_lo) << tshift);
-            tiles[tshift ? q : dense_rec(q)] = r;
+            tiles[q] = r;
         }
     // the wave's objects with many records, one after the other, 64 records per pass
     uint64_t big = __ballot(!own);
@@ -533,7 +527,7 @@ __global__ __launch_bounds__(256) void k_batch_map(const s3dg_obj_desc *d, uint6
         const uint64_t lo = readlane64(rec_lo, src), hi = readlane64(rec_hi, src);
         for (uint64_t q = lo + lane; q < hi; q += 64) {
             b.first = (uint32_t)((q - lo) << tshift);
-            tiles[tshift ? q : dense_rec(q)] = b;
+            tiles[q] = b;
         }
     }
 }
@@ -932,13 +926,7 @@ void launch_stream_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const u3
 template <int NT, int NW>
 void launch_batch_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *d, const TileRec *tiles,
                       uint64_t ntiles, uint64_t g0, uint32_t pf, uint32_t tshift, const u32x4 *b, uint32_t rt_floor) {
-    if (tshift == 0 && rt_floor)
-        hipLaunchKernelGGL((k_fill_batch<NT, NW, false, true, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0,
-                           pf, 0u, b, rt_floor);
-    else if (tshift == 0)
-        hipLaunchKernelGGL((k_fill_batch<NT, NW, false, false, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0,
-                           pf, 0u, b, 0u);
-    else if (rt_floor)
+    if (rt_floor)
         hipLaunchKernelGGL((k_fill_batch<NT, NW, false, true>), g, dim3(64 * NW), lds, s, d, tiles, ntiles, g0, pf,
                            tshift, b, rt_floor);
     else

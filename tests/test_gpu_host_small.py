@@ -1,7 +1,7 @@
 """GPU: the host-buffer engine's small calls and the generator read-ahead
 ring (round 4), byte for byte against the C oracle.
 
-* small calls (<= 4 MiB): the kernel stores straight into pinned host memory
+* small calls (<= 1 MiB; up to 16 MiB into library-pinned memory): the kernel stores straight into pinned host memory
   (the caller's when this library allocated it, else a bounce buffer copied
   out piece by piece).  Checked into pageable and library-pinned buffers,
   with guard bytes around the written range, for the fill_controlled_data

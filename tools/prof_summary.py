@@ -35,7 +35,7 @@ def bench_line(path):
 
 def is_step(name, kinds=STEP_KERNELS):
     """A step kernel, not the store-only reference (k_fill_batch<NT, NW, true, ...>: ABL, the third
-    template argument; the FLOOR and DENSE instantiations carry `true` in later positions)."""
+    template argument; the FLOOR instantiation carries `true` in the fourth)."""
     import re
     return any(k in name for k in kinds) and not re.search(r"k_fill_batch<\d+, \d+, true", name)
 
