@@ -379,9 +379,6 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 // rt_floor > 0).  The floor-free instantiation carries none of its code: the
 // conditional real-time read and wait cost launches that never use them
 // 0.3-1 % (round 4 library A/B).
-#ifndef S3DG_DIAG_LATEIMG
-#define S3DG_DIAG_LATEIMG 0
-#endif
 template <int NT, int NW, bool ABL = false, bool FLOOR = false>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
@@ -402,21 +399,19 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(raw) : "s"(tiles + tile) : "memory");
     u32x4 B[4 / NW];
     load_base<NW>(B, t, base);
-#if !S3DG_DIAG_LATEIMG
-    store_image<NW>(S, t, B);
-#endif
-    // the wait "redefines" raw, so no use of the record can move above it
+    // the wait "redefines" raw, so no use of the record can move above it.
+    // The LDS image is written after it (round 4): before, this wait also
+    // covered the image's ds_writes, which wait for the base block's loads,
+    // so the record-dependent work (and a dead slot's exit) started only once
+    // those had landed; after: config 2 +0.45-0.5 %, config 4 +0.2 %,
+    // config 3 -0.25 % (two library A/Bs, profiles/r04/d, profiles/r04/e).
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(raw) :: "memory");
     const TileRec e = __builtin_bit_cast(TileRec, raw);
     const uint32_t k = (uint32_t)(g & ((1u << tshift) - 1));
     const int64_t ib = (int64_t)e.first + k - e.lead;
     uint8_t *const bdst = dst_base + e.dst_off + (uint64_t)ib * kBlk;
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
-#if S3DG_DIAG_LATEIMG
-    // diagnostic (round 4): the LDS image written after the exit test, so a
-    // dead slot leaves without waiting for the base block's loads
     store_image<NW>(S, t, B);
-#endif
     if constexpr (ABL) {   // store-only reference: wave 0 idles `pace` x 2 x 64 cycles in the plan's place
         if (wave == 0)
             for (uint32_t q = 0; q < pace; ++q) __builtin_amdgcn_s_sleep(2);

@@ -34,16 +34,15 @@ b cfg18 --config 18 --steps 3 --warmup 1 --cpu-seconds 5
 b cfg18_pinned --config 18 --steps 3 --warmup 1 --host-mem pinned --cpu-seconds 5
 b cfg19 --config 19 --steps 3 --warmup 1 --cpu-seconds 5
 b cfg20 --config 20 --steps 3 --warmup 1 --cpu-seconds 5
-b cfg20_pin --config 20 --steps 3 --warmup 1 --cpu-seconds 5 --cpu-pin
 b cfg23 --config 23 --steps 3 --warmup 1 --cpu-seconds 5
-b cfg2 --config 2 --steps 10 --warmup 2
+b cfg2 --config 2 --steps 10 --warmup 2 --cpu-seconds 5
 b cfg2_pin --config 2 --steps 10 --warmup 2 --cpu-pin --no-d2h --no-ceiling
-b cfg3 --config 3 --steps 10 --warmup 2
-b cfg5 --config 5 --steps 3 --warmup 1
-b cfg8 --config 8 --steps 10 --warmup 2
-b cfg9 --config 9 --steps 10 --warmup 2
+b cfg3 --config 3 --steps 10 --warmup 2 --cpu-seconds 5
+b cfg5 --config 5 --steps 3 --warmup 1 --cpu-seconds 5
+b cfg8 --config 8 --steps 10 --warmup 2 --cpu-seconds 5 --no-ceiling
+b cfg9 --config 9 --steps 10 --warmup 2 --cpu-seconds 5 --no-ceiling
 step lib_ab
-LAB_AB="r03=dedd5d0;head=.;head_lateimg=.:-DS3DG_DIAG_LATEIMG=1" LAB_POINTS="cfg2;cfg3;cfg4;cfg10" LAB_REPS=12 \
+LAB_AB="r03=dedd5d0;head=.;head_lateimg=.:-DS3DG_DIAG_LATEIMG=1" LAB_POINTS="cfg2;cfg3;cfg4;cfg10" LAB_REPS=10 \
     timeout -k 10 500 python -u tools/r04/lib_ab.py > $OUT/lib_ab.log 2>&1 || exit 1
 grep -v "rep " $OUT/lib_ab.log
 step pmc
