@@ -379,9 +379,6 @@ __global__ __launch_bounds__(64 * NW) void k_fill_stream(uint8_t *dst, const u32
 // rt_floor > 0).  The floor-free instantiation carries none of its code: the
 // conditional real-time read and wait cost launches that never use them
 // 0.3-1 % (round 4 library A/B).
-#ifndef S3DG_DIAG_IMGPLAN
-#define S3DG_DIAG_IMGPLAN 0
-#endif
 template <int NT, int NW, bool ABL = false, bool FLOOR = false>
 __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const TileRec *tiles,
                                                         uint64_t ntiles, uint64_t g0, uint32_t pf,
@@ -408,27 +405,21 @@ __global__ __launch_bounds__(64 * NW) void k_fill_batch(uint8_t *dst_base, const
     // so the record-dependent work (and a dead slot's exit) started only once
     // those had landed; after: config 2 +0.45-0.5 %, config 4 +0.2 %,
     // config 3 -0.25 % (two library A/Bs, profiles/r04/d, profiles/r04/e).
+    // Later still, after wave 0's plan (gen_block's own image write), lost
+    // 3.5-5.7 % on configs 2, 4 and 5 (profiles/r04/g).
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(raw) :: "memory");
     const TileRec e = __builtin_bit_cast(TileRec, raw);
     const uint32_t k = (uint32_t)(g & ((1u << tshift) - 1));
     const int64_t ib = (int64_t)e.first + k - e.lead;
     uint8_t *const bdst = dst_base + e.dst_off + (uint64_t)ib * kBlk;
     if (ib < 0 || (uint64_t)ib * kBlk >= e.size) return;   // uniform for the whole workgroup
-#if !S3DG_DIAG_IMGPLAN
     store_image<NW>(S, t, B);
-#endif
     if constexpr (ABL) {   // store-only reference: wave 0 idles `pace` x 2 x 64 cycles in the plan's place
         if (wave == 0)
             for (uint32_t q = 0; q < pace; ++q) __builtin_amdgcn_s_sleep(2);
     }
-#if S3DG_DIAG_IMGPLAN
-    // diagnostic (round 4): the image written by gen_block after wave 0's plan
-    gen_block<NT, NW, false, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B, t0,
-                                  (!ABL && FLOOR) ? pace : 0u);
-#else
     gen_block<NT, NW, true, ABL>(bdst, S, t, wave, (uint32_t)ib, e.size, e.entropy, e.pp, B, t0,
                                  (!ABL && FLOOR) ? pace : 0u);
-#endif
     // one prefetching workgroup per XCD per span blocks (256: 128 and 512
     // measured slower); lane q of it touches the q-th
     // 128-byte line (2 records) of the span's records
