@@ -936,7 +936,7 @@ def pin_cpus(dev: int, n: int) -> list[int]:
     return (local + [c for c in aff if c not in local])[:n]
 
 
-def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=5, pin=False):
+def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=False):
     """The C restatement of the same generator (oracle, kind 'port') on this
     host's cores, parallel like the reference's Rayon loops: a warm-up sample,
     then `reps` samples of seconds/reps each, the median reported with min and
@@ -961,10 +961,14 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=5, pin=False):
             os.sched_setaffinity(0, saved)
     vals = sorted(r["value"] for r in runs)
     med = vals[len(vals) // 2]
+    q1, q3 = vals[len(vals) // 4], vals[(3 * len(vals)) // 4]
     out = dict(next(r for r in runs if r["value"] == med))
+    # spread: (max - min) / median; iqr_spread: (q3 - q1) / median, which a
+    # single sample disturbed by another job on the shared host does not move
     out.update(value=med, samples_GiBps=[r["value"] for r in runs],
-               min_med_max_GiBps=[vals[0], med, vals[-1]],
+               min_med_max_GiBps=[vals[0], med, vals[-1]], q1_q3_GiBps=[q1, q3],
                spread=round((vals[-1] - vals[0]) / med, 4) if med else None,
+               iqr_spread=round((q3 - q1) / med, 4) if med else None,
                pinned_cpus=f"{len(cpus)} CPUs: {cpus[0]}-{cpus[-1]}" if cpus else "no (scheduler's choice)",
                sample=f"median of {reps} samples; one sample: " + out["sample"])
     return out
