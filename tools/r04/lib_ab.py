@@ -14,7 +14,8 @@ batch floor compiled out and with round 2's 2^22-workgroup grid cap, flags
 since removed or kept as diagnostics: profiles/r04/lib_ab/).
 Points: cfg2 / cfg3 / cfg5 (10 000 x 8 MiB streams, d1 c1 / d4 c2 / d2 c3),
 cfg4 (10 000 log-uniform objects, d2 c1.5, batch), cfg10 (2 000 000 x
-(20 KiB + 5 B) at a 24 KiB stride, batch, dense layout).  Each sample is LAB_LAUNCHES
+(20 KiB + 5 B) at a 24 KiB stride, batch, dense layout), kb20g (2 000 000 x
+20 KiB at a 24 KiB stride: a dead gap slot per object).  Each sample is LAB_LAUNCHES
 back-to-back launches between two HIP events on one stream.
 Tooling only: nothing in the product imports this."""
 import ctypes, json, os, statistics, subprocess, sys, tarfile, io
@@ -102,6 +103,10 @@ def main():
     arr10 = (ObjDesc * n10)()
     for j in range(n10):
         arr10[j] = ObjDesc(j * 24576, 20 * 1024 + 5, SEED_BASE + (j << 32), 1, 0, 1)
+    # "kb20g": config 10's count of 20 KiB objects at a 24 KiB stride (a dead gap slot per object)
+    arr20g = (ObjDesc * n10)()
+    for j in range(n10):
+        arr20g[j] = ObjDesc(j * 24576, 20 * 1024, SEED_BASE + (j << 32), 1, 0, 1)
     buf = torch.empty(max(8 * MiB * n, off, n10 * 24576), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     sh = ctypes.c_void_p(st.cuda_stream)
@@ -110,6 +115,7 @@ def main():
     work = {k: 8 * MiB * n for k in streams}
     work["cfg4"] = sum(sizes)
     work["cfg10"] = n10 * (20 * 1024 + 5)
+    work["kb20g"] = n10 * 20 * 1024
 
     def run(L, h, kind):
         kind, _, split = kind.partition("@")      # "cfg4@64": s3dg_set_batch_split(64) for this point
@@ -120,6 +126,8 @@ def main():
             r = L.s3dg_fill_controlled_stream(h, p, 8 * MiB, 8 * MiB, n, d, fn, fd, SEED_BASE, 0, sh)
         elif kind == "cfg10":
             r = L.s3dg_fill_controlled_batch(h, p, arr10, n10, sh)
+        elif kind == "kb20g":
+            r = L.s3dg_fill_controlled_batch(h, p, arr20g, n10, sh)
         else:
             r = L.s3dg_fill_controlled_batch(h, p, arr, n, sh)
         assert r == 0, (kind, r)
