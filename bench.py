@@ -442,13 +442,15 @@ def main() -> int:
         kernel, launch_shape = "k_keystream", ("k_keystream<64,1>: 64 lanes x 4096 draws per 2 MiB chunk "
                                                "(jump-ahead, state sequence on the scalar unit), 64-draw LDS stage "
                                                "per lane, 512-B row pieces per store, 1-wave workgroups in XCD "
-                                               "groups of 16")
+                                               "groups of 16; a persistent grid over per-XCD unit queues from 6 "
+                                               "rounds of resident waves up")
     elif kind in ("dgen", "dgen_stream"):
         kernel, launch_shape = "k_keystream (DG1 mode)", (
             ("k_keystream<64,4>: 512 draws per lane, 256 lanes per 1 MiB DG1 block, zero-prefix waves skip "
              "the PRNG, XCD groups of 32 waves" if fn else
              "k_keystream<64,1>: 2048 draws per lane, 64 lanes per 1 MiB DG1 block, jump state sequence on the "
-             "scalar unit, XCD groups of 16 waves")
+             "scalar unit, XCD groups of 16 waves, a persistent grid over per-XCD unit queues from 6 rounds of "
+             "resident waves up")
             + ("; all objects of the step in one launch" if kind == "dgen_stream" else "; one launch per object"))
     else:
         batch = kind == "batch" or tiled

@@ -129,6 +129,13 @@ int s3dg_set_keystream_shape(s3dg_ctx *ctx, int mode, int draws, int waves, int 
  * default: 16, DG1 with a zero prefix 32).  A tuning knob; results are
  * identical. */
 int s3dg_set_keystream_xcd_group(s3dg_ctx *ctx, int mode, uint32_t waves);
+/* Keystream launches (both modes) of at least `rounds` rounds of resident
+ * waves run a persistent grid: one round of workgroups whose waves take work
+ * units from per-XCD queues (an XCD that runs ahead takes over units of a
+ * slower one instead of idling at the end of the launch).  0 = never; negative
+ * = default: 1-wave workgroups from 6 rounds.  A tuning knob; results are
+ * identical. */
+int s3dg_set_keystream_persist(s3dg_ctx *ctx, int rounds);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
 /* Resident workgroups per CU the current settings give (HIP occupancy API):
  * batch 0 = stream launches, 1 = batch launches, 2 = batch launches whose

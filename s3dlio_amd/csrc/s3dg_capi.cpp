@@ -162,6 +162,8 @@ struct StreamState {
         hipEvent_t consumed = nullptr;  // device copy may be freed (k_batch_map done; both on `up`)
     } stage[2];
     int next = 0;
+    // queue counters of persistent keystream launches on this stream
+    KsCounters ks;
     // lifetime (under the context's mu): users holding the state, and whether
     // s3dg_stream_release has taken it out of the context's map; the last
     // holder of a released state drains the stream and frees it
@@ -191,6 +193,7 @@ struct s3dg_ctx {
     KsShape ks[2] = {kDefaultKsShape[0], kDefaultKsShape[1]};
     uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
     bool ks_auto_waves[2] = {true, true}, ks_auto_xcd[2] = {true, true};          // not set by the caller
+    int ks_persist = -1;               // persistent keystream launches from this many rounds (-1: default)
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // tile maps and batch staging, one set per stream (s3dg::StreamState)
@@ -486,6 +489,7 @@ static void stream_state_free(StreamState *S) {
         if (G.consumed) (void)hipEventDestroy(G.consumed);
     }
     if (S->up) (void)hipStreamDestroy(S->up);
+    if (S->ks.dev) (void)hipFree(S->ks.dev);
     delete S;
 }
 
@@ -685,6 +689,13 @@ int s3dg_set_keystream_xcd_group(s3dg_ctx *c, int mode, uint32_t waves) {
     std::lock_guard<std::mutex> g(c->mu);
     c->ks[mode].xcd_waves = waves ? (int)waves : kDefaultKsXcdWaves;
     c->ks_auto_xcd[mode] = waves == 0;
+    return S3DG_OK;
+}
+
+int s3dg_set_keystream_persist(s3dg_ctx *c, int rounds) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->ks_persist = rounds < 0 ? -1 : rounds;
     return S3DG_OK;
 }
 
@@ -1309,6 +1320,24 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     return S3DG_OK;
 }
 
+// The stream's queue counters for persistent keystream launches, allocated
+// and zeroed on the stream's first keystream launch.  Caller holds S->mu.
+static int ks_counters(StreamState *S, KsCounters **out) {
+    if (!S->ks.dev) {
+        void *p = nullptr;
+        HIP_TRY(hipMalloc(&p, kKsCtrBytes), "hipMalloc(keystream counters)");
+        const hipError_t e = hipMemset(p, 0, kKsCtrBytes);
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            HIP_TRY(e, "hipMemset(keystream counters)");
+        }
+        S->ks.dev = (uint64_t *)p;
+        S->ks.par = 0;
+    }
+    *out = &S->ks;
+    return S3DG_OK;
+}
+
 int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes,
                       uint64_t seed_base, void *stream) {
     CTX_SCOPE(c);
@@ -1329,7 +1358,11 @@ int s3dg_xoshiro_fill(s3dg_ctx *c, void *dst, uint64_t len, uint64_t chunk_bytes
     A.m_unique = 0;
     A.zf_num = 0;
     A.zf_den = 1;
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, c->ks[0], (hipStream_t)stream), "launch k_keystream");
+    StreamLock SL(c, (hipStream_t)stream);
+    KsCounters *kc = nullptr;
+    if (int r = ks_counters(SL.get(), &kc)) return r;
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, c->ks[0], (hipStream_t)stream, kc, c->cus, c->ks_persist),
+            "launch k_keystream");
     return S3DG_OK;
 }
 
@@ -1388,7 +1421,11 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
         if (c->ks_auto_waves[1]) sh.waves = kDgenPrefixWaves;
         if (c->ks_auto_xcd[1]) sh.xcd_waves = kDgenPrefixXcdWaves;
     }
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, (hipStream_t)stream), "launch k_keystream(dgen)");
+    StreamLock SL(c, (hipStream_t)stream);
+    KsCounters *kc = nullptr;
+    if (int r = ks_counters(SL.get(), &kc)) return r;
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, (hipStream_t)stream, kc, c->cus, c->ks_persist),
+            "launch k_keystream(dgen)");
     return S3DG_OK;
 }
 

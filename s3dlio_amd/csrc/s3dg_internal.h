@@ -135,6 +135,21 @@ struct KeystreamArgs {
     // dealing): each full group of 8*xg workgroups is remapped so the xg
     // workgroups one XCD receives take xg adjacent work units
     uint32_t xg;
+    // set by launch_keystream: workgroups of the static grid; for a persistent
+    // launch (ks_ctr given, more than one round of resident waves) the stream's
+    // two sets of 8 queue counters (KsCounters) and the set this launch uses
+    uint32_t nwg;
+    uint32_t par;
+    uint64_t *ctr;
+};
+
+// Per-stream queue counters of persistent keystream launches: 2 sets x 8
+// counters, 128 B apart (kKsCtrBytes, zeroed at allocation); `par` alternates
+// per persistent launch, each launch zeroing the other set for the next.
+constexpr size_t kKsCtrBytes = 2 * 8 * 128;
+struct KsCounters {
+    uint64_t *dev = nullptr;
+    uint32_t par = 0;
 };
 
 // k_keystream launch shape: draws staged per lane per iteration (16, 32, 64),
@@ -145,8 +160,13 @@ struct KsShape {
     int store;             // kStorePlain / kStoreNT / kStoreSC1 / kStoreNTSC1
     int xcd_waves;         // adjacent waves per XCD group (power of two; <= waves: dealing order)
 };
+// ctrs: the stream's queue counters (persistent launches), or null for the
+// static grid.  cus: compute units of the device.  persist_rounds: launches
+// of at least that many rounds of resident waves run persistent (0: never;
+// negative: the default rule, 1-wave workgroups from kKsPersistRounds).
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
-                           const KsShape &sh, hipStream_t s);
+                           const KsShape &sh, hipStream_t s, KsCounters *ctrs = nullptr, int cus = 0,
+                           int persist_rounds = -1);
 hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu);
 
 // thr/nthr: records for the tiled shape's trailing loads (lc.prefetch_tiles), or null

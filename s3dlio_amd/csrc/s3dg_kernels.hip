@@ -23,6 +23,8 @@
 #include "s3dg_internal.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 // Diagnostic builds only (tools/ablate.py): bit 0 = no window patch phase,
 // bit 1 = no PRNG chain; k_keystream: bit 5 = no Xoshiro steps in the draw
@@ -619,36 +621,39 @@ __device__ __forceinline__ void xo_step(uint64_t &s0, uint64_t &s1, uint64_t &s2
     s0 = n0; s1 = n1; s2 = n2;
 }
 
+// Workgroups are dealt round-robin to the 8 XCDs, so consecutive ones write
+// through different L2s.  Each full group of 8*xg workgroups is remapped so
+// the xg workgroups one XCD receives take xg adjacent work units: every XCD
+// writes runs of xg*W*64 adjacent lane regions (the last,
+// partial group keeps the dealing order).  b: the workgroup's index in the
+// static grid of A.nwg workgroups (dealt to XCD b mod 8).
+__device__ __forceinline__ uint64_t ks_remap(const KeystreamArgs &A, uint64_t b) {
+    if (A.xg > 1) {
+        const uint32_t gs = (uint32_t)__builtin_ctz(A.xg);
+        if (((b >> (gs + 3)) + 1) << (gs + 3) <= A.nwg) {
+            const uint64_t x = b & 7, k = b >> 3;
+            return ((k >> gs) << (gs + 3)) + (x << gs) + (k & (A.xg - 1));
+        }
+    }
+    return b;
+}
+
+// One work unit: wave w of remapped workgroup bid, i.e. lanes
+// [(bid*W + w)*64, +64) of the launch.  myrows: this wave's LDS rows.
 template <int D, int W, int SP>
-__global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
+__device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
+                                        uint8_t *myrows, uint32_t l, uint64_t bid, uint32_t w) {
     static_assert(D == 16 || D == 32 || D == 64, "draws per stage");
     constexpr int RS = D * 8 + 16;     // row stride: + 16 B pad, conflict-light ds_write_b128 rows
     constexpr int P = D / 2;           // 16-byte pieces per row
     constexpr int R = 64 / P;          // rows per store instruction
-    __shared__ __attribute__((aligned(16))) uint8_t rows[W][64 * RS];
 #if S3DG_KS_TRACE
     const uint64_t t_start = wall_clock64();
 #endif
-    const uint32_t t = threadIdx.x, l = t & 63;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
-    uint8_t *myrows = rows[w];
     const uint32_t lpc = A.lpc, span = A.span;
     // global lane gl -> chunk gl / lpc, lane-in-chunk gl % lpc (lpc: power of two;
     // lpc > 64 spreads one chunk over lpc/64 waves)
     const uint32_t lsh = (uint32_t)__builtin_ctz(lpc);
-    // Workgroups are dealt round-robin to the 8 XCDs, so consecutive ones
-    // write through different L2s.  Each full group of 8*xg workgroups is
-    // remapped so the xg workgroups one XCD receives take xg adjacent work
-    // units: every XCD writes runs of xg*W*64 adjacent lane regions
-    // (the last, partial group keeps the dealing order).
-    uint64_t bid = blockIdx.x;
-    if (A.xg > 1) {
-        const uint32_t gs = (uint32_t)__builtin_ctz(A.xg);
-        if (((bid >> (gs + 3)) + 1) << (gs + 3) <= gridDim.x) {
-            const uint64_t x = bid & 7, k = bid >> 3;
-            bid = ((k >> gs) << (gs + 3)) + (x << gs) + (k & (A.xg - 1));
-        }
-    }
     const uint64_t gl = (bid * W + w) * 64 + l;
     const uint64_t c = gl >> lsh;                                    // local chunk index
     const uint64_t cpo = A.cpo ? A.cpo : A.nchunks;
@@ -858,11 +863,62 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
 #endif
 }
 
+// Persistent launches: the next work unit for a wave on XCD x.  Queue v holds
+// the wave units of the static grid's workgroups b = v (mod 8) in order
+// (q -> workgroup 8*(q/W) + v, wave q%W): the units XCD v would have been dealt.
+// A wave drains its own XCD's queue, then takes from the others', so an XCD
+// that runs ahead takes over the work of a slower one instead of idling at the
+// end of the launch.  One device-scope fetch-add (lane 0, vector memory) per
+// attempt; `gone` marks the queues found empty (wave-uniform).
+template <int W>
+__device__ __forceinline__ bool ks_take(const KeystreamArgs &A, uint64_t *ctr, uint32_t x, uint32_t l,
+                                        uint32_t &gone, uint64_t &b, uint32_t &w) {
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t v = (x + i) & 7;
+        if (gone & (1u << v)) continue;
+        const uint64_t quota = (uint64_t)W * ((A.nwg + 7 - v) / 8);
+        uint64_t q = 0;
+        if (l == 0) q = __hip_atomic_fetch_add(ctr + 16 * v, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        q = readlane64(q, 0);
+        if (q < quota) {
+            b = 8 * (q / W) + v;
+            w = (uint32_t)(q % W);
+            return true;
+        }
+        gone |= 1u << v;
+    }
+    return false;
+}
+
+// Keystream launch.  Static grid (A.ctr null): workgroup blockIdx.x does its
+// own W units.  Persistent (A.ctr set, launches of more than one round of
+// resident waves): gridDim.x workgroups stay resident and every wave takes
+// units from the per-XCD queues until all are empty; counter set A.par of
+// A.ctr serves this launch, and workgroup 0 zeroes the other set for the next
+// launch on the stream (launches on one stream never overlap).
+template <int D, int W, int SP>
+__global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
+    constexpr int RS = D * 8 + 16;
+    __shared__ __attribute__((aligned(16))) uint8_t rows[W][64 * RS];
+    const uint32_t t = threadIdx.x, l = t & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+    uint8_t *myrows = rows[w];
+    if (!A.ctr) {
+        ks_unit<D, W, SP>(dst, A, jtab, myrows, l, ks_remap(A, blockIdx.x), w);
+        return;
+    }
+    uint64_t *const cur = A.ctr + (A.par ? 128 : 0);   // 8 counters, 128 B apart
+    if (blockIdx.x == 0 && t < 8)
+        __hip_atomic_store(A.ctr + (A.par ? 0 : 128) + 16 * t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x = blockIdx.x & 7;
+    uint32_t gone = 0, ww = 0;
+    uint64_t b = 0;
+    while (ks_take<W>(A, cur, x, l, gone, b, ww)) ks_unit<D, W, SP>(dst, A, jtab, myrows, l, ks_remap(A, b), ww);
+}
+
 template <int D, int W>
 hipError_t launch_ks_one(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab, uint32_t lds,
-                         int store, hipStream_t s) {
-    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
-    const uint64_t wgs = (waves + W - 1) / W;
+                         int store, hipStream_t s, uint64_t wgs) {
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (store == kStoreSC1)
         hipLaunchKernelGGL((k_keystream<D, W, kStoreSC1>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
@@ -1081,14 +1137,70 @@ hipError_t launch_fill_uniform_tiles_ablated(const LaunchCfg &lc, uint8_t *dst, 
     return batch_tiles(lc, dst, total_tiles, tshift, tiles, base_dev, s, true);
 }
 
+// Persistent keystream launches from this many rounds of resident waves up.
+// Whole libraries in one process, interleaved: persistent
+// for any launch of more than one round against the static grid
+// (profiles/r04/k/pass1/lib_ab.log): one 80 GiB DG1 launch 6715 -> 7011 GB/s,
+// K2 84 GB in one launch 6763 -> 7087, ten 8 GiB DG1 launches (8 rounds each)
+// 6248 -> 6441, but K2 8 GiB launches (4 rounds of 4096-draw lanes)
+// 6417 -> 6388 and DG1 with a zero prefix (4-wave workgroups, short
+// all-zero units) 6204 -> 6018.  From 6 rounds, 1-wave workgroups only
+// (profiles/r04/k/lib_ab.log): the three gains kept (6421 / 6987 / 7052
+// against 6232 / 6646 / 6705), 4-round launches unchanged (persistent from
+// one round: DG1 4 GiB launches 6175 -> 6151, K2 8 GiB 6400 -> 6376).
+#ifndef S3DG_KS_PERSIST_ROUNDS
+#define S3DG_KS_PERSIST_ROUNDS 6
+#endif
+constexpr uint32_t kKsPersistRounds = S3DG_KS_PERSIST_ROUNDS;
+
+// Resident workgroups per CU of a keystream shape (cached: the occupancy
+// query is a host-side calculation, but a host call's latency budget is µs).
+static int ks_resident_per_cu(const KsShape &sh, uint32_t lds) {
+    static std::mutex mu;
+    static std::map<uint64_t, int> cache;
+    const uint64_t key = ((uint64_t)sh.draws << 48) | ((uint64_t)sh.waves << 40) | lds;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    hipError_t e;
+    S3DG_KS_DISPATCH(e, occ_ks_one, sh, lds, &n);
+    if (e != hipSuccess) n = 0;
+    (void)hipGetLastError();
+    cache[key] = n;
+    return n;
+}
+
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A0, const uint64_t *jtab,
-                           const KsShape &sh, hipStream_t s) {
+                           const KsShape &sh, hipStream_t s, KsCounters *ctrs, int cus, int persist_rounds) {
     (void)hipGetLastError();
     const uint32_t lds = occupancy_lds(sh.wgs_per_cu, ks_static_lds(sh.draws, sh.waves));
     KeystreamArgs A = A0;
     A.xg = sh.xcd_waves > sh.waves ? (uint32_t)(sh.xcd_waves / sh.waves) : 1u;
+    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
+    const uint64_t wgs = (waves + sh.waves - 1) / sh.waves;
+    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    A.nwg = (uint32_t)wgs;
+    A.ctr = nullptr;
+    A.par = 0;
+    uint64_t grid = wgs;
+#if !S3DG_DIAG_KS_STATIC
+    // at least `rounds` rounds of resident waves (default: 1-wave workgroups
+    // from kKsPersistRounds): a persistent grid over per-XCD queues
+    // (k_keystream), one resident round of workgroups, a multiple of 8
+    const uint64_t rounds = persist_rounds < 0 ? (sh.waves == 1 ? kKsPersistRounds : 0) : (uint64_t)persist_rounds;
+    if (rounds > 0 && ctrs && ctrs->dev && cus > 0) {
+        const uint64_t cap = ((uint64_t)ks_resident_per_cu(sh, lds) * (uint64_t)cus) & ~7ull;
+        if (cap >= 8 && wgs >= rounds * cap) {
+            A.ctr = ctrs->dev;
+            A.par = ctrs->par;
+            grid = cap;
+        }
+    }
+#endif
     hipError_t e;
-    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s);
+    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s, grid);
+    if (e == hipSuccess && A.ctr) ctrs->par ^= 1u;
     return e;
 }
 

@@ -202,6 +202,12 @@ class Context:
         lane regions (power of two; 0 = default 16); results are identical."""
         call("s3dg_set_keystream_xcd_group", self._h, int(mode), int(waves))
 
+    def set_keystream_persist(self, rounds: int = -1) -> None:
+        """Keystream launches of >= `rounds` rounds of resident waves run a
+        persistent grid over per-XCD work queues (0 = never, negative = default:
+        1-wave workgroups from 6 rounds).  Results are identical."""
+        call("s3dg_set_keystream_persist", self._h, int(rounds))
+
     def query_keystream_occupancy(self, mode: int = 0) -> int:
         out = ctypes.c_int()
         call("s3dg_query_keystream_occupancy", self._h, int(mode), ctypes.byref(out))

@@ -15,7 +15,11 @@ since removed or kept as diagnostics: profiles/r04/lib_ab/).
 Points: cfg2 / cfg3 / cfg5 (10 000 x 8 MiB streams, d1 c1 / d4 c2 / d2 c3),
 cfg4 (10 000 log-uniform objects, d2 c1.5, batch), cfg10 (2 000 000 x
 (20 KiB + 5 B) at a 24 KiB stride, batch, dense layout), kb20g (2 000 000 x
-20 KiB at a 24 KiB stride: a dead gap slot per object).  Each sample is LAB_LAUNCHES
+20 KiB at a 24 KiB stride: a dead gap slot per object); keystream points
+cfg14 / cfg15 (ten 8 GiB DG1 launches, d1 c1 / d2 c2), cfg16 (the ten in one
+launch), cfg6 (K2, 10 000 x 8 MiB as 2 MiB chunks, one launch), k2_8g (the
+same keystream as 8 GiB launches; k2_8g_2048 with 2048-draw lanes), dg1_4g
+(twenty 4 GiB DG1 c1 launches).  Each sample is LAB_LAUNCHES
 back-to-back launches between two HIP events on one stream.
 Tooling only: nothing in the product imports this."""
 import ctypes, json, os, statistics, subprocess, sys, tarfile, io
@@ -89,6 +93,10 @@ def main():
         L.s3dg_fill_controlled_stream.argtypes = [ctypes.c_void_p] * 2 + [u64] * 4 + [u32] * 2 + [u64] * 2 + [
             ctypes.c_void_p]
         L.s3dg_fill_controlled_batch.argtypes = [ctypes.c_void_p] * 3 + [u64, ctypes.c_void_p]
+        L.s3dg_dgen_fill.argtypes = [ctypes.c_void_p] * 2 + [u64] * 4 + [u32] * 2 + [u64, ctypes.c_void_p]
+        L.s3dg_dgen_fill_stream.argtypes = [ctypes.c_void_p] * 2 + [u64] * 4 + [u32] * 2 + [u64] * 2 + [
+            ctypes.c_void_p]
+        L.s3dg_xoshiro_fill.argtypes = [ctypes.c_void_p] * 2 + [u64] * 3 + [ctypes.c_void_p]
         h = ctypes.c_void_p()
         assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
         libs[name] = (L, h)
@@ -107,7 +115,7 @@ def main():
     arr20g = (ObjDesc * n10)()
     for j in range(n10):
         arr20g[j] = ObjDesc(j * 24576, 20 * 1024, SEED_BASE + (j << 32), 1, 0, 1)
-    buf = torch.empty(max(8 * MiB * n, off, n10 * 24576), dtype=torch.uint8, device="cuda")
+    buf = torch.empty(max(8 * MiB * n, off, n10 * 24576, 10 << 33), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     sh = ctypes.c_void_p(st.cuda_stream)
     p = ctypes.c_void_p(buf.data_ptr())
@@ -117,10 +125,42 @@ def main():
     work["cfg10"] = n10 * (20 * 1024 + 5)
     work["kb20g"] = n10 * 20 * 1024
 
+    G8 = 8 << 30
+    ks_pts = {"cfg14": (1, 0, 1), "cfg15": (2, 1, 2)}   # DG1 d, f_num, f_den: ten 8 GiB launches
+    for k in ("cfg14", "cfg15", "cfg16", "cfg6", "k2_8g", "k2_8g_2048", "dg1_4g"):
+        work[k] = 10 * G8 if k != "cfg6" else 8 * MiB * n
+
     def run(L, h, kind):
         kind, _, split = kind.partition("@")      # "cfg4@64": s3dg_set_batch_split(64) for this point
         if hasattr(L, "s3dg_set_batch_split"):
             assert L.s3dg_set_batch_split(h, int(split) if split else -1) == 0
+        if kind in ks_pts:                        # configs 14/15: one s3dg_dgen_fill per 8 GiB object
+            d, fn, fd = ks_pts[kind]
+            for t in range(10):
+                assert L.s3dg_dgen_fill(h, ctypes.c_void_p(buf.data_ptr() + t * G8), u64(G8), u64(0), u64(1 << 40),
+                                        u64(d), u32(fn), u32(fd), u64(SEED_BASE + t), sh) == 0
+            return
+        if kind == "cfg16":                       # ten 8 GiB DG1 objects in one launch
+            assert L.s3dg_dgen_fill_stream(h, p, u64(G8), u64(G8), u64(10), u64(1), u32(0), u32(1),
+                                           u64(SEED_BASE), u64(0), sh) == 0
+            return
+        if kind == "cfg6":                        # K2: 10 000 x 8 MiB as 2 MiB chunks, one launch
+            assert L.s3dg_xoshiro_fill(h, p, u64(8 * MiB * n), u64(2 * MiB), u64(0), sh) == 0
+            return
+        if kind == "dg1_4g":                      # twenty 4 GiB DG1 c1 launches (4 rounds each)
+            for t in range(20):
+                assert L.s3dg_dgen_fill(h, ctypes.c_void_p(buf.data_ptr() + t * (G8 // 2)), u64(G8 // 2), u64(0),
+                                        u64(1 << 40), u64(1), u32(0), u32(1), u64(SEED_BASE + t), sh) == 0
+            return
+        if kind in ("k2_8g", "k2_8g_2048"):       # the same keystream as 8 GiB launches
+            if kind == "k2_8g_2048":              # 2048-draw lanes (8 rounds) instead of 4096 (4)
+                assert L.s3dg_set_keystream_shape(h, 0, 0, 0, 0, u64(2048), -1) == 0
+            for t in range(10):
+                assert L.s3dg_xoshiro_fill(h, ctypes.c_void_p(buf.data_ptr() + t * G8), u64(G8), u64(2 * MiB),
+                                           u64(t * (G8 // (2 * MiB))), sh) == 0
+            if kind == "k2_8g_2048":
+                assert L.s3dg_set_keystream_shape(h, 0, 0, 0, 0, u64(0), -1) == 0
+            return
         if kind in streams:
             d, fn, fd = streams[kind]
             r = L.s3dg_fill_controlled_stream(h, p, 8 * MiB, 8 * MiB, n, d, fn, fd, SEED_BASE, 0, sh)
