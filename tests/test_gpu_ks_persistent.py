@@ -131,3 +131,37 @@ def test_persist_knob_off_and_bad_args(S):
     c.set_keystream_persist(0)
     c.set_keystream_persist(-5)      # default rule
     c.set_keystream_persist(3)
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_persistent_fuzz_shapes(S, gpu_ctx, case):
+    """Seeded draws of object size (1.1-2.3 GiB, ragged), dedup, compress,
+    workgroup waves, XCD group and lane length, DG1 or K2, through a context
+    that runs every launch of one round or more persistent; bytes equal the
+    default context's static pieces of less than one round."""
+    import random
+    import torch
+    rng = random.Random(9000 + case)
+    c = S.Context(0, base_seed=S.DEFAULT_BASE_SEED)
+    c.set_keystream_persist(1)
+    mode = rng.choice((0, 1))
+    waves = rng.choice((1, 2, 4))
+    c.set_keystream_shape(mode, 64, waves, 0, rng.choice((512, 1024, 2048)), -1)
+    c.set_keystream_xcd_group(mode, rng.choice((1, 4, 16, 64)))
+    size = int(rng.uniform(1.1, 2.3) * GiB) + rng.randrange(1, 4096)
+    a = torch.full((size + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    b = torch.full_like(a, 0xAB)
+    if mode == 1:
+        d, cc, seed = rng.choice((1, 2, 3)), rng.choice((1, 2, 3)), rng.getrandbits(64)
+        c.dgen_fill(a, size, dedup=d, compress=cc, seed=seed)
+        c.dgen_fill(a, size, dedup=d, compress=cc, seed=seed)
+        _pieces_dgen(gpu_ctx, b, size, d, cc, seed)
+    else:
+        size = size // 16 * 16
+        sb = rng.getrandbits(40)
+        c.xoshiro_fill(a, size, seed_base=sb)
+        per = 128 * 2 * MiB
+        for off in range(0, size, per):
+            gpu_ctx.xoshiro_fill(b[off:], min(per, size - off), seed_base=sb + off // (2 * MiB))
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), (mode, waves, size)
