@@ -8,6 +8,8 @@ persistent launches on one stream (the queue counter sets alternate) and on
 two streams.  A context with s3dg_set_keystream_persist(1) forces the
 persistent grid from one round up (both workgroup shapes); the default rule
 (1-wave workgroups from 6 rounds) is covered at 6 GiB."""
+import os
+
 import numpy as np
 import pytest
 
@@ -133,12 +135,13 @@ def test_persist_knob_off_and_bad_args(S):
     c.set_keystream_persist(3)
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(int(os.environ.get("S3DG_PERSIST_FUZZ", "8"))))
 def test_persistent_fuzz_shapes(S, gpu_ctx, case):
     """Seeded draws of object size (1.1-2.3 GiB, ragged), dedup, compress,
     workgroup waves, XCD group and lane length, DG1 or K2, through a context
     that runs every launch of one round or more persistent; bytes equal the
-    default context's static pieces of less than one round."""
+    default context's static pieces of less than one round.  S3DG_PERSIST_FUZZ
+    sets the number of draws (default 8)."""
     import random
     import torch
     rng = random.Random(9000 + case)
