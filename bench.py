@@ -564,6 +564,7 @@ def main() -> int:
                     "kernel": kernel, "launch_shape": launch_shape,
                     "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": algo_per_launch,
+                    "launch_ms_distribution": launch_distribution(kern_ms),
                     "source_digest": src_digest, "library_digest": lib_digest}
         if kind in ("stream", "batch"):
             # the zero-class setting the context measured and chose (s3dg_query_zero_tune)
@@ -611,6 +612,21 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     cp.close()
     return 0
+
+
+def launch_distribution(ms: list) -> dict:
+    """Per-launch HIP-event times of the timed steps (the mean is
+    what the line scores, and a bimodal run shows here): mean, p10/p50/p90,
+    max, and the share of launches slower than 1.06 x p10."""
+    v = sorted(ms)
+    if not v:
+        return {}
+
+    def pct(q):
+        return round(v[min(len(v) - 1, int(q * len(v)))], 4)
+    p10 = v[min(len(v) - 1, int(0.1 * len(v)))]
+    return {"n": len(v), "mean": round(sum(v) / len(v), 4), "p10": pct(0.1), "p50": pct(0.5), "p90": pct(0.9),
+            "max": round(v[-1], 4), "slow_share_over_1.06xp10": round(sum(x > 1.06 * p10 for x in v) / len(v), 4)}
 
 
 def host_buffer(n: int, kind: str, call):

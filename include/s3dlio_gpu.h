@@ -136,6 +136,16 @@ int s3dg_set_keystream_xcd_group(s3dg_ctx *ctx, int mode, uint32_t waves);
  * = default: 1-wave workgroups from 6 rounds.  A tuning knob; results are
  * identical. */
 int s3dg_set_keystream_persist(s3dg_ctx *ctx, int rounds);
+/* DG1 launches with a zero prefix (compress > 1) of at least `chunks` whole
+ * 1 MiB blocks (all of them full length) run as two launches: the blocks'
+ * zero prefixes in the fill's store shape (whole 4 KiB granules, every XCD on
+ * every 8th), then the keystream over the blocks' tails only.  chunks: 0 =
+ * always one keystream launch, negative = default (64).  The zero launch:
+ * `waves` per 4 KiB workgroup (1, 2, 4), `occupancy` resident workgroups per
+ * CU cap (0 = none), `store` policy (as s3dg_set_store_policy), `overlap` 1 =
+ * on a side stream concurrent with the tails (the caller's stream waits for
+ * both); negative = default for each.  A tuning knob; results are identical. */
+int s3dg_set_dgen_zero_split(s3dg_ctx *ctx, int chunks, int waves, int occupancy, int store, int overlap);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
 /* Resident workgroups per CU the current settings give (HIP occupancy API):
  * batch 0 = stream launches, 1 = batch launches, 2 = batch launches whose

@@ -112,16 +112,33 @@ def build(force: bool = False, verbose: bool = False) -> str:
     build_native_loop(force, verbose)
     if not force and not _stale():
         return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
-           # kernel arguments preloaded into SGPRs (gfx950): the first scalar
-           # load of every 4 KiB-block workgroup disappears from its critical path
-           "-mllvm", "-amdgpu-kernarg-preload-count=16",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
-           "-DS3DG_BUILD", f"-DS3DG_BUILD_DIGEST=\"{source_digest()}\"", "-o", LIB] + SOURCES
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+             # kernel arguments preloaded into SGPRs (gfx950): the first scalar
+             # load of every 4 KiB-block workgroup disappears from its critical path
+             "-mllvm", "-amdgpu-kernarg-preload-count=16",
+             "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+             "-DS3DG_BUILD", f"-DS3DG_BUILD_DIGEST=\"{source_digest()}\""]
+    # one translation unit per process (no device code crosses units), then link
+    import concurrent.futures as cf
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="s3dg_obj_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in SOURCES]
+
+        def compile_one(k):
+            cmd = [HIPCC, *flags, "-c", "-o", objs[k], SOURCES[k]]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.check_call(cmd)
+        workers = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0")) or os.cpu_count() or 1))
+        with cf.ThreadPoolExecutor(workers) as pool:
+            list(pool.map(compile_one, range(len(SOURCES))))
+        tmp_lib = LIB + ".tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib] + objs
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(tmp_lib, LIB)
     return LIB
 
 

@@ -134,6 +134,14 @@ constexpr int kDefaultKsXcdWaves = 16;
 constexpr KsShape kDefaultKsShape[2] = {{64, 1, 0, kStoreSC1, kDefaultKsXcdWaves},
                                         {64, 1, 0, kStoreSC1, kDefaultKsXcdWaves}};
 constexpr int kDgenPrefixWaves = 4, kDgenPrefixXcdWaves = 32;
+// DG1 with a zero prefix, from this many whole 1 MiB blocks per launch: the
+// prefixes as whole 4 KiB granules in the fill's store shape (k_zero_prefix),
+// then the keystream over the tails alone (s3dg_set_dgen_zero_split;
+// DESIGN.md §5.3).  The zero launch's occupancy cap and store policy.
+constexpr uint64_t kDefaultDgenZeroSplit = 64;
+constexpr int kDefaultZeroPrefixWaves = 1, kDefaultZeroPrefixOcc = 0;
+constexpr int kDefaultZeroPrefixStore = kStoreSC1;
+constexpr int kDefaultZeroPrefixOverlap = 0;   // 1: the zero launch on a side stream, concurrent with the tails
 
 // Launch state private to one stream: the tile-record map of tiled launches
 // and the batch-descriptor staging.  Launches on one stream are ordered by
@@ -152,6 +160,9 @@ struct StreamState {
     hipEvent_t filled[2] = {nullptr, nullptr};   // fill reading map [i] done (on the stream)
     int bnext = 0;
     hipStream_t up = nullptr;          // batch entry uploads + record maps (overlap the previous fill)
+    // DG1 zero-prefix launches concurrent with their tails (s3dg_set_dgen_zero_split overlap)
+    hipStream_t zs = nullptr;
+    hipEvent_t zfork = nullptr, zjoin = nullptr;
     struct Stage {
         s3dg_obj_desc *host = nullptr, *dev = nullptr;   // pinned staging / device copy
         uint64_t *rec_lo = nullptr;    // device: record offset of each object (tile layouts)
@@ -194,12 +205,15 @@ struct s3dg_ctx {
     uint64_t ks_min_draws[2] = {kDefaultKsMinDraws[0], kDefaultKsMinDraws[1]};   // draws per lane
     bool ks_auto_waves[2] = {true, true}, ks_auto_xcd[2] = {true, true};          // not set by the caller
     int ks_persist = -1;               // persistent keystream launches from this many rounds (-1: default)
+    uint64_t dgen_zero_split = kDefaultDgenZeroSplit;   // DG1 zero prefix + tail launches from this many blocks
+    int zp_waves = kDefaultZeroPrefixWaves, zp_occ = kDefaultZeroPrefixOcc, zp_store = kDefaultZeroPrefixStore;
+    int zp_overlap = kDefaultZeroPrefixOverlap;
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // tile maps and batch staging, one set per stream (s3dg::StreamState)
     std::map<hipStream_t, StreamState *> streams;
     int stream_tiles = kDefaultStreamTiles;   // uniform streams through the tiled batch kernel
-    std::map<uint64_t, uint64_t *> jtabs;   // (lpc << 32 | span) -> device jump table
+    std::map<std::pair<uint64_t, uint64_t>, uint64_t *> jtabs;   // (lpc << 32 | span, z0) -> device jump table
     void *crc_tab = nullptr;           // slicing-by-8 tables (device)
     uint32_t *crc_seg = nullptr;       // per-segment CRCs (device)
     uint64_t crc_seg_cap = 0;
@@ -489,6 +503,9 @@ static void stream_state_free(StreamState *S) {
         if (G.consumed) (void)hipEventDestroy(G.consumed);
     }
     if (S->up) (void)hipStreamDestroy(S->up);
+    if (S->zs) (void)hipStreamDestroy(S->zs);
+    for (hipEvent_t e : {S->zfork, S->zjoin})
+        if (e) (void)hipEventDestroy(e);
     if (S->ks.dev) (void)hipFree(S->ks.dev);
     delete S;
 }
@@ -534,6 +551,7 @@ int s3dg_stream_release(s3dg_ctx *c, void *stream) {
         std::lock_guard<std::mutex> g(S->mu);    // wait for an enqueue in progress
         e = hipStreamSynchronize((hipStream_t)stream);
         if (e == hipSuccess && S->up) e = hipStreamSynchronize(S->up);
+        if (e == hipSuccess && S->zs) e = hipStreamSynchronize(S->zs);
     }
     bool last;
     {
@@ -699,6 +717,21 @@ int s3dg_set_keystream_persist(s3dg_ctx *c, int rounds) {
     return S3DG_OK;
 }
 
+int s3dg_set_dgen_zero_split(s3dg_ctx *c, int chunks, int waves, int occupancy, int store, int overlap) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    if (waves != 0 && waves != 1 && waves != 2 && waves != 4 && waves >= 0)
+        return fail(S3DG_EINVAL, "waves must be 1, 2 or 4 (0 or negative: default)");
+    if (occupancy > 64) return fail(S3DG_EINVAL, "occupancy must be <= 64 workgroups per CU");
+    if (store > kStoreNTSC1) return fail(S3DG_EINVAL, "store policy must be 0, 1, 2, 3 or negative");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->dgen_zero_split = chunks < 0 ? kDefaultDgenZeroSplit : (uint64_t)chunks;
+    c->zp_waves = waves <= 0 ? kDefaultZeroPrefixWaves : waves;
+    c->zp_occ = occupancy < 0 ? kDefaultZeroPrefixOcc : occupancy;
+    c->zp_store = store < 0 ? kDefaultZeroPrefixStore : store;
+    c->zp_overlap = overlap < 0 ? kDefaultZeroPrefixOverlap : (overlap ? 1 : 0);
+    return S3DG_OK;
+}
+
 int s3dg_query_keystream_occupancy(s3dg_ctx *c, int mode, int *wgs_per_cu) {
     CTX_SCOPE(c);
     if (!wgs_per_cu || (mode != 0 && mode != 1)) return fail(S3DG_EINVAL, "bad argument");
@@ -741,6 +774,7 @@ public:
         if (last) {
             (void)hipStreamSynchronize(s_);
             if (S_->up) (void)hipStreamSynchronize(S_->up);
+            if (S_->zs) (void)hipStreamSynchronize(S_->zs);
             stream_state_free(S_);
         }
     }
@@ -1251,17 +1285,19 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         LaunchCfg lcs = cfg_for(c, true, cand ? kZcNone : zcls);
         if (tshift == 0) lcs.store = c->store_dense;
         if (timed) tune_mark(c, zcls, probe, false, s);
+        hipError_t le;
         if (ms) {
-            HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs_s, tsh_s, S->btiles[tb], c->base_dev, s),
-                    "launch k_fill_batch");
-            HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs - recs_s, tsh_l, S->btiles[tb] + recs_s,
-                                       c->base_dev, s),
-                    "launch k_fill_batch");
+            le = launch_batch_tiles(lcs, (uint8_t *)dst_base, recs_s, tsh_s, S->btiles[tb], c->base_dev, s);
+            if (le == hipSuccess)
+                le = launch_batch_tiles(lcs, (uint8_t *)dst_base, recs - recs_s, tsh_l, S->btiles[tb] + recs_s,
+                                        c->base_dev, s);
         } else {
-            HIP_TRY(launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s),
-                    "launch k_fill_batch");
+            le = launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s);
         }
+        // the probe's end mark even when a launch failed: its events go back
+        // to the tuner (harvested later) instead of leaking
         if (timed) tune_mark(c, zcls, probe, true, s);
+        HIP_TRY(le, "launch k_fill_batch");
         HIP_TRY(hipEventRecord(S->filled[tb], s), "hipEventRecord");
         k0 = k1;
     }
@@ -1277,9 +1313,11 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
 }
 
 // lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
+// z0 > 0: the lanes cover draws [z0, chunk_bytes / 8) of every chunk (the
+// tails of a DG1 zero-prefix split), one wave per tail when it has >= 64 x 256 draws.
 static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t nchunks, bool zero_prefix,
-                          KeystreamArgs &A, const uint64_t **jtab) {
-    const uint64_t nd = chunk_bytes / 8;
+                          KeystreamArgs &A, const uint64_t **jtab, uint64_t z0 = 0) {
+    const uint64_t nd = chunk_bytes / 8 - z0;
     // as many lanes per chunk as keep >= ks_min_draws draws per lane (the
     // jump costs 256 steps); up to 1024 lanes = 16 waves per chunk
     uint64_t min_draws = c->ks_min_draws[mode];
@@ -1292,6 +1330,8 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     }
     uint32_t lpc = 1;
     while (lpc < 1024 && nd / (2 * lpc) >= min_draws) lpc *= 2;
+    // a tail: 64 lanes (one wave, the jump's state sequence on the scalar unit)
+    if (z0 && lpc < 64 && nd >= 64 * kKsMinSpan) lpc = 64;
     // small launches (a few chunks): spread each chunk over more lanes, down
     // to 256 draws per lane, until the grid has ~4 waves per CU; otherwise a
     // 8 MiB request runs as 16 long waves and is latency-bound
@@ -1303,13 +1343,14 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     if (span > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "chunk too large");
     A.lpc = lpc;
     A.span = (uint32_t)span;
+    A.z0 = z0;
     std::lock_guard<std::mutex> g(c->mu);
-    const uint64_t key = ((uint64_t)lpc << 32) | span;
+    const std::pair<uint64_t, uint64_t> key{((uint64_t)lpc << 32) | span, z0};
     auto it = c->jtabs.find(key);
     if (it == c->jtabs.end()) {
         std::vector<uint64_t> h(4 * (size_t)lpc, 0);
         for (uint32_t k = 0; k < lpc; ++k)
-            if (!jump_poly((uint64_t)k * span, &h[4 * k]))
+            if (!jump_poly(z0 + (uint64_t)k * span, &h[4 * k]))
                 return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
         uint64_t *d = nullptr;
         HIP_TRY(hipMalloc(&d, h.size() * 8), "hipMalloc(jump table)");
@@ -1399,9 +1440,28 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     if (n_objs > 1 && stride < span_bytes) return fail(S3DG_EINVAL, "stride too small: objects overlap");
     if (f_den == 0 || f_num >= f_den) return fail(S3DG_EINVAL, "need f_num < f_den");
     if (nb > 0xFFFFFFFFull) return fail(S3DG_EINVAL, "object larger than 2^32 blocks");
+    // zero prefix + tail split: every block of the launch full length, the
+    // prefix at least 8 whole granules, enough blocks to pay for two launches
+    uint64_t split;
+    LaunchCfg zlc;
+    bool overlap;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        split = c->dgen_zero_split;
+        zlc.store = c->zp_store;
+        zlc.waves_per_block = c->zp_waves;
+        zlc.dyn_lds = occupancy_lds(c->zp_occ, 0);
+        overlap = c->zp_overlap != 0;
+    }
+    const uint64_t nchunks = (blk_hi - blk_lo) * n_objs;
+    const uint32_t zg = (uint32_t)(kDgenBlock * f_num / f_den / kBlk);
+    const bool zsplit = f_num > 0 && split && nchunks >= split && zg >= 8 &&
+                        (obj_size % kDgenBlock == 0 || blk_hi < nb);
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, 1, kDgenBlock, (blk_hi - blk_lo) * n_objs, f_num > 0, A, &jt)) return r;
+    if (int r = keystream_plan(c, 1, kDgenBlock, nchunks, f_num > 0 && !zsplit, A, &jt,
+                               zsplit ? (uint64_t)zg * (kBlk / 8) : 0))
+        return r;
     const uint64_t U = s3dg_unique_blocks(nb, dedup);
     A.cpo = blk_hi - blk_lo;
     A.nchunks = A.cpo * n_objs;
@@ -1417,15 +1477,30 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     A.zf_num = f_num;
     A.zf_den = f_den;
     KsShape sh = c->ks[1];
-    if (f_num > 0) {   // zero-prefix launches (512-draw lanes): 4-wave workgroups, groups of 32 waves
+    if (f_num > 0 && !zsplit) {   // zero-prefix launches (512-draw lanes): 4-wave workgroups, groups of 32 waves
         if (c->ks_auto_waves[1]) sh.waves = kDgenPrefixWaves;
         if (c->ks_auto_xcd[1]) sh.xcd_waves = kDgenPrefixXcdWaves;
     }
     StreamLock SL(c, (hipStream_t)stream);
     KsCounters *kc = nullptr;
     if (int r = ks_counters(SL.get(), &kc)) return r;
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, (hipStream_t)stream, kc, c->cus, c->ks_persist),
-            "launch k_keystream(dgen)");
+    hipStream_t s = (hipStream_t)stream;
+    StreamState *SS = SL.get();
+    if (zsplit && !overlap) {   // the prefixes' whole granules first (the tail launch masks a partial one)
+        HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zg, zlc, s),
+                "launch k_zero_prefix");
+    } else if (zsplit) {        // on the side stream, concurrent with the tails (disjoint bytes)
+        if (!SS->zs) HIP_TRY(hipStreamCreateWithFlags(&SS->zs, hipStreamNonBlocking), "hipStreamCreate(zero)");
+        for (hipEvent_t *e : {&SS->zfork, &SS->zjoin})
+            if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+        HIP_TRY(hipEventRecord(SS->zfork, s), "hipEventRecord");
+        HIP_TRY(hipStreamWaitEvent(SS->zs, SS->zfork, 0), "hipStreamWaitEvent");
+        HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zg, zlc, SS->zs),
+                "launch k_zero_prefix");
+        HIP_TRY(hipEventRecord(SS->zjoin, SS->zs), "hipEventRecord");
+    }
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, s, kc, c->cus, c->ks_persist), "launch k_keystream(dgen)");
+    if (zsplit && overlap) HIP_TRY(hipStreamWaitEvent(s, SS->zjoin, 0), "hipStreamWaitEvent");
     return S3DG_OK;
 }
 

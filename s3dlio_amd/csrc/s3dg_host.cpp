@@ -276,10 +276,16 @@ bool pinned_owned(const void *p, uint64_t n) {
     // and HIP still knows it as pinned host memory (a registry entry outlives a
     // buffer freed behind the library's back; a kernel must never store into
     // pageable memory: without XNACK that is a GPU page fault)
-    hipPointerAttribute_t at{};
-    const bool pinned = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
-    (void)hipGetLastError();
-    return pinned;
+    // at both ends of the range: a registry entry whose buffer was freed and
+    // whose start address a smaller pinned allocation reuses passes at p
+    // alone
+    auto host_pinned = [](const void *q) {
+        hipPointerAttribute_t at{};
+        const bool ok = hipPointerGetAttributes(&at, q) == hipSuccess && at.type == hipMemoryTypeHost;
+        (void)hipGetLastError();
+        return ok;
+    };
+    return host_pinned(p) && (n <= 1 || host_pinned((const uint8_t *)p + (n - 1)));
 }
 
 hipError_t host_alloc_pinned_local(int device, uint64_t bytes, void **out) {

@@ -141,7 +141,19 @@ struct KeystreamArgs {
     uint32_t nwg;
     uint32_t par;
     uint64_t *ctr;
+    // first draw of every chunk the launch covers (lane sub starts at draw
+    // z0 + sub*span; jtab[sub] = x^(z0 + sub*span)): a DG1 launch over the
+    // chunks' tails whose zero prefixes k_zero_prefix has written
+    uint64_t z0;
 };
+
+// DG1 zero prefixes in the fill's store shape (paired with a keystream launch
+// over the tails, A.z0 > 0): the first zg whole 4 KiB granules of each of
+// nchunks chunks (chunk c of object c / cpo at dst + (c / cpo)*obj_stride +
+// (c % cpo)*chunk_bytes) set to zero; one workgroup of 64 x lc.waves_per_block
+// threads per granule, lc.store, lc.dyn_lds capping the resident workgroups.
+hipError_t launch_zero_prefix(uint8_t *dst, uint64_t nchunks, uint64_t cpo, uint64_t obj_stride, uint64_t chunk_bytes,
+                              uint32_t zg, const LaunchCfg &lc, hipStream_t s);
 
 // Per-stream queue counters of persistent keystream launches: 2 sets x 8
 // counters, 128 B apart (kKsCtrBytes, zeroed at allocation); `par` alternates

@@ -667,7 +667,8 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
     const uint64_t clen = (c < A.nchunks && gofs < A.obj_len)
                               ? ((A.obj_len - gofs) < A.chunk_bytes ? (A.obj_len - gofs) : A.chunk_bytes)
                               : 0;
-    const uint64_t rb = (uint64_t)sub * span * 8;                    // lane region within chunk
+    const uint64_t d0 = A.z0 + (uint64_t)sub * span;                 // first draw index
+    const uint64_t rb = d0 * 8;                                      // lane region within chunk
     const uint32_t rlen = (uint32_t)(clen > rb ? ((clen - rb) < (uint64_t)span * 8 ? (clen - rb) : (uint64_t)span * 8) : 0);
     const uint64_t tail_draw = clen >> 3;                            // draw index of a 1..7 B tail
     const bool tail_hi = (clen & 7) >= 1 && (clen & 7) <= 4;         // next_u32 = next_u64 >> 32
@@ -685,7 +686,6 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
     }
     uint64_t s0 = mix64(x + 0x9E3779B97F4A7C15ull), s1 = mix64(x + 2 * 0x9E3779B97F4A7C15ull);
     uint64_t s2 = mix64(x + 3 * 0x9E3779B97F4A7C15ull), s3 = mix64(x + 4 * 0x9E3779B97F4A7C15ull);
-    const uint64_t d0 = (uint64_t)sub * span;                        // first draw index
     const uint32_t iters = span / D;
     const uint32_t piece = l % P;
     // destination of the P rows this lane helps write: row R*i + l/P, piece l%P
@@ -728,7 +728,8 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
         // is wave-uniform: it runs on the scalar unit (64-bit s_xor/s_lshl,
         // SGPRs) and each lane only accumulates the states its own jump
         // polynomial selects (8 v_bitop3 with an SGPR operand per step, was
-        // 8 + the 11-op vector step).  Lane sub = 0 has J = 1: a = s.
+        // 8 + the 11-op vector step).  Lane sub = 0 of a launch with z0 = 0
+        // has J = 1: a = s.
         uint64_t u0 = readlane64(s0, 0), u1 = readlane64(s1, 0);
         uint64_t u2 = readlane64(s2, 0), u3 = readlane64(s3, 0);
         // the lane's 256-bit polynomial in two loads up front (one load and
@@ -751,7 +752,7 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
             }
         }
         s0 = a0; s1 = a1; s2 = a2; s3 = a3;
-    } else if (lpc > 1 && sub > 0) {             // jump to draw sub*span
+    } else if (A.z0 || (lpc > 1 && sub > 0)) {   // jump to draw z0 + sub*span
         // state <- sum over set bits i of J of step^i(state): 256 steps, the
         // polynomial read as 8 32-bit halves so each step's mask is one
         // sign-extended bit field and each accumulate one v_bitop3
@@ -914,6 +915,39 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     uint32_t gone = 0, ww = 0;
     uint64_t b = 0;
     while (ks_take<W>(A, cur, x, l, gone, b, ww)) ks_unit<D, W, SP>(dst, A, jtab, myrows, l, ks_remap(A, b), ww);
+}
+
+// DG1 zero prefixes in the fill's store shape (paired with a keystream launch
+// over the chunks' tails, s3dg_internal_dgen_chunk): one 64-thread workgroup
+// per 4 KiB granule, four 16-byte zero stores per lane (1 KiB per
+// instruction).  2D grid: x = granule of the chunk, padded to zgp (a multiple
+// of 8), y = chunk, so the linear workgroup id y*zgp + x, dealt round-robin
+// to the XCDs, lands on XCD x mod 8 and writes granule x of its chunk, = x
+// (mod 8) in the buffer: every XCD on every 8th granule, as the fill
+// (DESIGN.md §5.1).  The dgen keystream's own all-zero waves write 64 lane
+// regions per wave instead (§5.2).  Chunk y -> object y / cpo by Lemire's
+// fastdiv (m_cpo = floor(2^64 / cpo) + 1; y, cpo < 2^32).
+template <int SP, int NW>
+__global__ __launch_bounds__(64 * NW) void k_zero_prefix(uint8_t *dst, uint64_t y0, uint64_t cpo, uint64_t m_cpo,
+                                                         uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zg) {
+    const uint32_t x = blockIdx.x;
+    if (x >= zg) return;
+    const uint64_t y = y0 + blockIdx.y;
+    const uint64_t ko = __umul64hi(m_cpo, y);
+    const uint64_t cl = y - ko * cpo;
+    uint64_t off = ko * obj_stride + cl * chunk_bytes + (uint64_t)x * kBlk;
+    asm volatile("" : "+v"(off));   // the address on the VALU
+    uint8_t *p = dst + off + threadIdx.x * 16;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4 / NW; ++k) store16<SP>(p + k * 1024 * NW, z);
+}
+
+template <int SP, int NW>
+void launch_zp_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *dst, uint64_t y0, uint64_t cpo, uint64_t m_cpo,
+                   uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zg) {
+    hipLaunchKernelGGL((k_zero_prefix<SP, NW>), g, dim3(64 * NW), lds, s, dst, y0, cpo, m_cpo, obj_stride,
+                       chunk_bytes, zg);
 }
 
 template <int D, int W>
@@ -1209,6 +1243,24 @@ hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu) {
     hipError_t e;
     S3DG_KS_DISPATCH(e, occ_ks_one, sh, lds, wgs_per_cu);
     return e;
+}
+
+hipError_t launch_zero_prefix(uint8_t *dst, uint64_t nchunks, uint64_t cpo, uint64_t obj_stride, uint64_t chunk_bytes,
+                              uint32_t zg, const LaunchCfg &lc, hipStream_t s) {
+    (void)hipGetLastError();
+    if (zg == 0 || nchunks == 0) return hipSuccess;
+    if (cpo == 0 || cpo > 0xFFFFFFFFull || nchunks > 0xFFFFFFFFull || (chunk_bytes & 4095u) ||
+        (uint64_t)zg * kBlk > chunk_bytes)
+        return hipErrorInvalidValue;
+    const uint32_t zgp = (zg + 7u) & ~7u;
+    const uint64_t m_cpo = ~0ull / cpo + 1;
+    for (uint64_t y0 = 0; y0 < nchunks; y0 += 65535) {
+        const dim3 g(zgp, (uint32_t)((nchunks - y0) < 65535 ? (nchunks - y0) : 65535));
+        S3DG_DISPATCH(launch_zp_one, lc, g, lc.dyn_lds, s, dst, y0, cpo, m_cpo, obj_stride, chunk_bytes, zg);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_write_ceiling(const LaunchCfg &lc, uint8_t *dst, uint64_t len, uint32_t pattern,

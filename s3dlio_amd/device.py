@@ -208,6 +208,15 @@ class Context:
         1-wave workgroups from 6 rounds).  Results are identical."""
         call("s3dg_set_keystream_persist", self._h, int(rounds))
 
+    def set_dgen_zero_split(self, chunks: int = -1, waves: int = -1, occupancy: int = -1, store: int = -1,
+                            overlap: int = -1) -> None:
+        """DG1 launches with a zero prefix over >= `chunks` full 1 MiB blocks run
+        as a zero-prefix launch in the fill's store shape plus a keystream
+        launch over the tails (0 = never, negative = default 64); `waves`,
+        `occupancy`, `store` and `overlap` (side stream) tune the zero launch.
+        Results are identical."""
+        call("s3dg_set_dgen_zero_split", self._h, int(chunks), int(waves), int(occupancy), int(store), int(overlap))
+
     def query_keystream_occupancy(self, mode: int = 0) -> int:
         out = ctypes.c_int()
         call("s3dg_query_keystream_occupancy", self._h, int(mode), ctypes.byref(out))

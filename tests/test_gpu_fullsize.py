@@ -6,6 +6,11 @@ config 4) into HBM exactly as bench.py does; the oracle regenerates it on the
 host threads in 2 GiB windows, each window is uploaded and compared on the
 device with torch.equal.  Config 5 (100 000 objects, 839 GB) is checked whole,
 as ten 10 000-object ring passes (bench.py's N=1 ring).
+
+Every buffer is poisoned (0xA5) before the fill, so a block the kernel never
+wrote cannot pass for one a previous fill left behind, and the stream
+configurations sit between two 64 MiB guard regions that must still hold the
+poison afterwards (no store outside the objects).
 """
 import concurrent.futures as cf
 import ctypes
@@ -20,6 +25,8 @@ MiB = 1 << 20
 SEED_BASE = 0x5EED000000000001        # bench.py / SURVEY.md §8d
 BASE_SEED = 0xBA5EB10C00000000
 WINDOW = 2 << 30
+GUARD = 64 * MiB
+POISON = 0xA5
 THREADS = max(1, min(16, os.cpu_count() or 1))
 
 
@@ -49,16 +56,20 @@ def test_stream_config_every_byte(env, cfg, n, first, d, c):
     torch, S, OC, ctx, base, host, chk = env
     size = 8 * MiB
     fn, fd = P.compress_ratio(c)
-    dev = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    whole = torch.empty(n * size + 2 * GUARD, dtype=torch.uint8, device="cuda")
+    whole.fill_(POISON)
+    dev = whole[GUARD:GUARD + n * size]
     ctx.fill_stream(dev, obj_size=size, n_objs=n, dedup=d, compress=c, seed_base=SEED_BASE, first_obj=first)
     torch.cuda.synchronize()
+    assert int((whole[:GUARD] != POISON).sum()) == 0, "store before the buffer"
+    assert int((whole[GUARD + n * size:] != POISON).sum()) == 0, "store past the buffer"
     per = WINDOW // size
     hnp = host.numpy()
     for s0 in range(0, n, per):
         k = min(per, n - s0)
         OC.fill_stream(size, k, d, fn, fd, SEED_BASE, first + s0, base, threads=THREADS, out=hnp[:k * size])
         assert _compare(torch, host, chk, dev[s0 * size:(s0 + k) * size], k * size), (cfg, s0)
-    del dev
+    del dev, whole
 
 
 def test_batch_config4_every_byte(env):
@@ -72,6 +83,7 @@ def test_batch_config4_every_byte(env):
         offs.append(cur)
         cur += (sz + 4095) // 4096 * 4096
     dev = torch.empty(cur, dtype=torch.uint8, device="cuda")
+    dev.fill_(POISON)
     ctx.fill_batch(dev, [(offs[j], sizes[j], P.object_entropy(SEED_BASE, j), 2, (3, 2)) for j in range(n)])
     torch.cuda.synchronize()
     lib = OC.lib()
@@ -107,6 +119,7 @@ def test_keystream_config6_every_byte(env):
     torch, S, OC, ctx, base, host, chk = env
     total, chunk = 10000 * 8 * MiB, 2 * MiB
     dev = torch.empty(total, dtype=torch.uint8, device="cuda")
+    dev.fill_(POISON)
     ctx.xoshiro_fill(dev, total, chunk_bytes=chunk, seed_base=0)
     torch.cuda.synchronize()
     lib = OC.lib()

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One parameterized GPU-box session (replaces the one-shot tools/r0*/gpu_*.sh
+# scripts of rounds 2-4).  Run from the repository root:
+#
+#   gpurun -- 'bash tools/gpu_session.sh <out-dir> <step> [<step> ...]'
+#
+# Steps, each under its own time limit; the session stops at the first
+# failure (no GPU step runs after a fault, abort or time-out):
+#   tests[:EXPR]        pytest -m gpu (optionally -k EXPR), log gpu_tests.log
+#   file:PATH           pytest -m gpu on one test file
+#   smoke               __graft_entry__.smoke()
+#   bench:CFG[:ARGS]    bench.py --config CFG --steps 20 --warmup 5 ARGS (':'-separated)
+#   driver              bench.py with no flags (the driver's own command)
+#   prof:CFG            rocprofv3 --kernel-trace --stats of bench.py --config CFG
+#   pmc:CFG:COUNTER     one rocprofv3 --pmc pass (WRITE_SIZE or FETCH_SIZE) of bench.py --config CFG
+#   lab:SCRIPT[:ENV]    python tools/SCRIPT with ENV (comma-separated K=V) set
+# Environment: STEPS (bench steps, default 20), WARMUP (default 5).
+set -o pipefail
+OUT=gpurun_out/${1:?out dir}
+shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS=${STEPS:-20}
+WARMUP=${WARMUP:-5}
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+n=0
+for step in "$@"; do
+    n=$((n + 1))
+    IFS=':' read -r kind a b c <<< "$step"
+    tag=$(printf '%02d_%s' $n "$kind${a:+_$a}" | tr '/ ,=.' '_____')
+    echo "== $step ($tag)"
+    case "$kind" in
+    tests)
+        timeout -k 10 1100 $PYT tests ${a:+-k "$a"} > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -3 "$OUT/$tag.log";;
+    file)
+        timeout -k 10 600 $PYT "$a" > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -3 "$OUT/$tag.log";;
+    smoke)
+        timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -2 "$OUT/$tag.log";;
+    bench)
+        extra=$(echo "${b}${c:+:$c}" | tr ':' ' ')
+        timeout -k 10 400 python -u bench.py --config "$a" --steps "$STEPS" --warmup "$WARMUP" $extra \
+            > "$OUT/$tag.log" 2>&1; rc=$?
+        grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
+    driver)
+        timeout -k 10 400 python -u bench.py > "$OUT/$tag.log" 2>&1; rc=$?
+        grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
+    prof)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/$tag" -o run --output-format csv \
+            -- python3 bench.py --config "$a" --steps "$STEPS" --warmup "$WARMUP" --no-ceiling --no-d2h \
+            --no-cpu-baseline > "$OUT/$tag.log" 2>&1; rc=$?
+        grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-300;;
+    pmc)
+        timeout -s KILL 240 rocprofv3 --pmc "$b" -d "$OUT/$tag" -o run --output-format csv \
+            -- python3 bench.py --config "$a" --steps 3 --warmup 1 --no-ceiling --no-d2h --no-cpu-baseline \
+            --no-verify > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -1 "$OUT/$tag.log";;
+    lab)
+        envs=$(echo "$b" | tr ',' ' ')
+        timeout -k 10 900 env $envs python -u "tools/$a" > "$OUT/$tag.log" 2>&1; rc=$?
+        grep '^{' "$OUT/$tag.log" | cut -c1-400 | tail -40;;
+    *)
+        echo "unknown step $step"; rc=2;;
+    esac
+    if [ $rc -ne 0 ]; then
+        echo "step $step failed rc=$rc"; tail -30 "$OUT/$tag.log"; exit $rc
+    fi
+done
+echo "session ok"

@@ -4,8 +4,8 @@
 by side, each with its own context, and timed on the same workloads with the
 library defaults, interleaved, variant order rotated every round.
 
-    python tools/r04/lib_ab.py --build        # here: builds tools/_build/libab_<name>.so
-    python tools/r04/lib_ab.py                # GPU box: runs LAB_POINTS x variants
+    python tools/lib_ab.py --build        # here: builds tools/_build/libab_<name>.so
+    python tools/lib_ab.py                # GPU box: runs LAB_POINTS x variants
 
 Variants (LAB_AB, "name=git-ref|.[:-Dflag ...];..."): git-ref = the sources
 of that commit (git archive), "." = this tree.  Default: r02 final (aa93058),
@@ -21,10 +21,18 @@ launch), cfg6 (K2, 10 000 x 8 MiB as 2 MiB chunks, one launch), k2_8g (the
 same keystream as 8 GiB launches; k2_8g_2048 with 2048-draw lanes), dg1_4g
 (twenty 4 GiB DG1 c1 launches).  Each sample is LAB_LAUNCHES
 back-to-back launches between two HIP events on one stream.
+
+Per-launch mode (the driver scores the MEAN, and a
+median hides a slow mode): LAB_BLOCK=B times every launch with its own event
+pair, B launches back to back per variant per rep (as bench.py's steps run),
+and reports per variant the mean, p10/p50/p90/max and the share of launches
+slower than LAB_SLOW x the fastest variant's p10 (default 1.06); LAB_SMI=1
+polls the GPU's GFX clock and socket power (amdsmi, every ~5 ms) and gives
+the medians seen during the slow and the normal launches of each variant.
 Tooling only: nothing in the product imports this."""
 import ctypes, json, os, statistics, subprocess, sys, tarfile, io
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
 DEFAULT = "r02=aa93058;r03=dedd5d0;head=."
@@ -177,6 +185,27 @@ def main():
     res = {}
     digests = {}
     reps = int(os.environ.get("LAB_REPS", "8"))
+    block = int(os.environ.get("LAB_BLOCK", "0"))   # > 0: per-launch events, B launches per variant per rep
+    per = {}                                        # (variant, point) -> [(ms, t_start_host, t_end_host)]
+    rows, on, th = [], [True], None
+    if block and os.environ.get("LAB_SMI") == "1":
+        import threading, time
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from zero_power_lab import smi_handle
+        smi, sm, bdf = smi_handle()
+        print(json.dumps({"smi_device": bdf}), flush=True)
+
+        def poller():
+            while on[0]:
+                try:
+                    m = smi.amdsmi_get_gpu_metrics_info(sm)
+                    rows.append((time.perf_counter(), m.get("current_gfxclk"), m.get("current_socket_power")))
+                except Exception:  # noqa: BLE001
+                    pass
+                time.sleep(0.005)
+        th = threading.Thread(target=poller, daemon=True)
+        th.start()
+    import time
     for rep in range(reps):
         for k in pts:
             order = names[rep % len(names):] + names[:rep % len(names)]
@@ -186,24 +215,79 @@ def main():
                 L, h = libs[name]
                 run(L, h, k)
                 torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(st)
-                for _ in range(launches):
-                    run(L, h, k)
-                e1.record(st)
-                torch.cuda.synchronize()
-                res.setdefault((name, k), []).append(launches * work[k.partition("@")[0]] /
-                                                    (e0.elapsed_time(e1) * 1e-3) / 1e9)
+                if block:
+                    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                           for _ in range(block)]
+                    for e0, e1 in evs:
+                        e0.record(st)
+                        run(L, h, k)
+                        e1.record(st)
+                    t_end = []
+                    for _, e1 in evs:       # host stamp of each launch's end (lags by the sync latency)
+                        e1.synchronize()
+                        t_end.append(time.perf_counter())
+                    for q, (e0, e1) in enumerate(evs):
+                        ms = e0.elapsed_time(e1)
+                        per.setdefault((name, k), []).append((ms, t_end[q - 1] if q else t_end[q] - ms / 1e3,
+                                                              t_end[q]))
+                        res.setdefault((name, k), []).append(work[k.partition("@")[0]] / (ms * 1e-3) / 1e9)
+                else:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    for _ in range(launches):
+                        run(L, h, k)
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                    res.setdefault((name, k), []).append(launches * work[k.partition("@")[0]] /
+                                                        (e0.elapsed_time(e1) * 1e-3) / 1e9)
                 if rep == 0:   # every variant writes the same bytes
                     digests.setdefault(k, {})[name] = int(buf[:64 * MiB].to(torch.int64).sum().item())
         print(f"rep {rep} done", flush=True)
+    on[0] = False
+    if th:
+        th.join()
+    slow_x = float(os.environ.get("LAB_SLOW", "1.06"))
+
+    def pct(v, q):
+        v = sorted(v)
+        return v[min(len(v) - 1, int(q * len(v)))]
     for k in pts:
         same = len(set(digests[k].values())) == 1
         print(json.dumps({"point": k, "outputs_identical": same}), flush=True)
+        if block:
+            fastest = min(pct([m for m, _, _ in per[(n_, k)]], 0.1) for n_ in names)
+            thr = slow_x * fastest
         for name in names:
             v = res[(name, k)]
-            print(json.dumps({"variant": name, "point": k, "GBps_median": round(statistics.median(v), 1),
-                              "min": round(min(v), 1), "max": round(max(v), 1), "n": len(v)}), flush=True)
+            out = {"variant": name, "point": k, "GBps_median": round(statistics.median(v), 1),
+                   "min": round(min(v), 1), "max": round(max(v), 1), "n": len(v)}
+            if block:
+                ms = [m for m, _, _ in per[(name, k)]]
+                mean_ms = sum(ms) / len(ms)
+                slow = [i for i, m in enumerate(ms) if m > thr]
+                out.update({"GBps_mean": round(work[k.partition("@")[0]] / (mean_ms * 1e-3) / 1e9, 1),
+                            "ms_mean": round(mean_ms, 4), "ms_p10": round(pct(ms, 0.1), 4),
+                            "ms_p50": round(pct(ms, 0.5), 4), "ms_p90": round(pct(ms, 0.9), 4),
+                            "ms_max": round(max(ms), 4), "slow_threshold_ms": round(thr, 4),
+                            "slow_share": round(len(slow) / len(ms), 4)})
+                if rows:
+                    def during(ids):
+                        clk, pw = [], []
+                        for i in ids:
+                            _, a, b = per[(name, k)][i]
+                            for r in rows:
+                                if a < r[0] <= b:
+                                    if isinstance(r[1], (int, float)):
+                                        clk.append(r[1])
+                                    if isinstance(r[2], (int, float)):
+                                        pw.append(r[2])
+                        return {"launches": len(ids), "gfxclk_med": statistics.median(clk) if clk else None,
+                                "gfxclk_min": min(clk) if clk else None,
+                                "power_med": statistics.median(pw) if pw else None, "samples": len(clk)}
+                    fast = [i for i in range(len(ms)) if i not in set(slow)]
+                    out["smi_normal"] = during(fast)
+                    out["smi_slow"] = during(slow)
+            print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
