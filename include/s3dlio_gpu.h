@@ -164,13 +164,14 @@ int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
 int s3dg_zero_class(uint32_t f_num, uint32_t f_den);
 /* Batch-kernel launches of zero class 2 (above) check their store floor by
  * measurement: the context times its own launches of >= 1 GiB and runs the
- * floor or a plain launch, whichever wrote faster (best of each one's last
- * three rates, after two launches of each), re-probing the other every 16
- * launches; class 1 keeps its cap.  An explicit s3dg_set_occupancy /
- * s3dg_set_batch_pace (or env S3DG_ZC_TUNE=0) turns this off.  Query (zclass
- * 0-2): the choice (0 = the class setting, 1 = plain), each one's best recent
- * GB/s (0 = not measured yet) and the timed launch count.  Results are
- * identical. */
+ * floor or a plain launch (medians of each one's last five rates, after four
+ * launches of each; the other is taken only when more than 1 % faster than
+ * the current choice, so near-equal candidates do not flip between runs),
+ * re-probing the other every 32 launches; class 1 keeps its cap.  An
+ * explicit s3dg_set_occupancy / s3dg_set_batch_pace (or env S3DG_ZC_TUNE=0)
+ * turns this off.  Query (zclass 0-2): the choice (0 = the class setting, 1 =
+ * plain), each one's median recent GB/s (0 = not measured yet) and the timed
+ * launch count.  Results are identical. */
 int s3dg_query_zero_tune(s3dg_ctx *ctx, int zclass, int *best, double *rule_gbs, double *plain_gbs,
                          uint64_t *timed);
 /* Per-object entropy of object j of a stream: seed_base + j * 2^32. */
@@ -256,6 +257,16 @@ int s3dg_host_alloc_pinned(uint64_t bytes, void **out);
  * does not say).  Free with s3dg_host_free_pinned. */
 int s3dg_host_alloc_pinned_local(int device, uint64_t bytes, void **out);
 int s3dg_host_free_pinned(void *p);
+/* With env S3DLIO_HOST_REGISTER=1, a pageable buffer passed twice with the
+ * same address and length to a host-buffer call (s3dlio_fill_controlled_data
+ * and the other host entry points; whole 4 KiB blocks, 16-byte aligned, up to
+ * 16 MiB) is page-locked (hipHostRegister) and from then on written by the
+ * kernel directly, as s3dg_host_alloc_pinned memory.  Such a buffer must stay
+ * allocated until this call releases it (buf inside it; NULL = every
+ * registered buffer) or the process exits: freed while registered, the GPU
+ * would keep writing its old pages.  At most 64 buffers / 4 GiB at once.
+ * Returns the number of buffers released (>= 0). */
+int s3dg_host_unregister(void *buf);
 /* NUMA node of `device` from sysfs (-1 when unknown). */
 int s3dg_device_numa_node(int device, int *node);
 int s3dg_d2h_async(s3dg_ctx *ctx, void *host, const void *dev, uint64_t len, void *stream);

@@ -19,6 +19,7 @@ hipError_t crc32_device(const uint8_t *dev, uint64_t len, hipStream_t s, uint32_
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <memory>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -67,15 +68,20 @@ enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
 // differs between boxes.  So a context times its own large launches of that
 // class (HIP events around the fill, read back without waiting, at a later
 // launch) and runs the floor or the plain uncapped launch, whichever wrote
-// faster: the best of each one's last kTuneKeep rates, after kTuneFirst
-// launches of each (a process's first launch is slow), probing the loser
-// again every kTuneReprobe launches.  The line-aligned class keeps its cap
-// unmeasured: it won 4-9 % on every box.  Launches below kTuneMinBytes use
-// the current choice; an explicit s3dg_set_occupancy / s3dg_set_batch_pace
-// (or S3DG_ZC_TUNE=0) turns the check off.
+// faster: after kTuneFirst launches of each (alternating; a process's first
+// launch is slow), the medians of each one's last kTuneKeep rates, the plain
+// launch taken only when it beats the current choice's median by more than
+// kTuneMargin (the class setting otherwise), so two candidates within the
+// noise of each other do not flip from run to run (the
+// best-of-3 rule did); the loser is probed again every kTuneReprobe launches.
+// The line-aligned class keeps its cap unmeasured: it won 4-9 % on every box.
+// Launches below kTuneMinBytes use the current choice; an explicit
+// s3dg_set_occupancy / s3dg_set_batch_pace (or S3DG_ZC_TUNE=0) turns the
+// check off.
 constexpr uint64_t kTuneMinBytes = 1ull << 30;
-constexpr uint64_t kTuneReprobe = 16;
-constexpr int kTuneKeep = 3, kTuneFirst = 2;
+constexpr uint64_t kTuneReprobe = 32;
+constexpr int kTuneKeep = 5, kTuneFirst = 4;
+constexpr double kTuneMargin = 0.01;
 struct ZcTuner {
     int best = 0;                  // 0 = the fitted rule, 1 = uncapped, no floor
     uint64_t launches = 0;         // timed launches issued
@@ -308,6 +314,16 @@ bool tune_enabled() {
     return on;
 }
 
+// Median rate (GB/s) of candidate q's last kTuneKeep timed launches (0: none).
+double tune_median(const ZcTuner &T, int q) {
+    const int n = std::min(T.samples[q], kTuneKeep);
+    if (n == 0) return 0.0;
+    double v[kTuneKeep];
+    std::copy(T.recent[q], T.recent[q] + n, v);
+    std::sort(v, v + n);
+    return n & 1 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
+}
+
 // A launch of class zc writing `bytes`: the candidate to run (0 = the fitted
 // rule, 1 = plain) and whether to time it (*timed, events in *probe).
 int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending *probe) {
@@ -335,10 +351,9 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
         T.pend.pop_back();
     }
     if (T.samples[0] >= kTuneFirst && T.samples[1] >= kTuneFirst) {
-        double top[2] = {0, 0};
-        for (int q = 0; q < 2; ++q)
-            for (int k = 0; k < kTuneKeep && k < T.samples[q]; ++k) top[q] = std::max(top[q], T.recent[q][k]);
-        T.best = top[1] > top[0] ? 1 : 0;
+        const double med[2] = {tune_median(T, 0), tune_median(T, 1)};
+        // switch only when the other candidate is clearly faster (hysteresis)
+        if (med[1 - T.best] > med[T.best] * (1.0 + kTuneMargin)) T.best = 1 - T.best;
     }
     if (bytes < kTuneMinBytes) return T.best;
     const int cand = T.issued[0] < (uint64_t)kTuneFirst || T.issued[1] < (uint64_t)kTuneFirst
@@ -663,12 +678,9 @@ int s3dg_query_zero_tune(s3dg_ctx *c, int zclass, int *best, double *rule_gbs, d
     if (!c || zclass < 0 || zclass > 2) return fail(S3DG_EINVAL, "bad argument");
     std::lock_guard<std::mutex> g(c->mu);
     const ZcTuner &T = c->tune[zclass];
-    double top[2] = {0, 0};
-    for (int q = 0; q < 2; ++q)
-        for (int k = 0; k < kTuneKeep && k < T.samples[q]; ++k) top[q] = std::max(top[q], T.recent[q][k]);
     if (best) *best = T.best;
-    if (rule_gbs) *rule_gbs = top[0];
-    if (plain_gbs) *plain_gbs = top[1];
+    if (rule_gbs) *rule_gbs = tune_median(T, 0);
+    if (plain_gbs) *plain_gbs = tune_median(T, 1);
     if (timed) *timed = T.launches;
     return S3DG_OK;
 }
@@ -807,8 +819,10 @@ static int tiles_reserve(StreamState *S, uint64_t tiles, hipStream_t s) {
 // ((first_obj + j) << 32), prefix parameters pp.  Large streams whose objects
 // all start on the same 4 KiB granule (mod 8) run through the tiled batch
 // kernel; the rest through the 2D stream kernel.
+// held: the stream's state when the caller already holds it (batch sub-batches).
 static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t stride, uint64_t n_objs,
-                        const PrefixParams &pp, uint64_t seed_base, uint64_t first_obj, hipStream_t s) {
+                        const PrefixParams &pp, uint64_t seed_base, uint64_t first_obj, hipStream_t s,
+                        StreamState *held = nullptr) {
     const uint64_t nb = (obj_size + kBlk - 1) / kBlk;
     const uint32_t lead = (uint32_t)(((uintptr_t)dst >> 12) & 7);
     if (c->stream_tiles && (n_objs == 1 || stride % (8 * kBlk) == 0) && n_objs * nb >= kStreamTilesMinBlocks &&
@@ -818,8 +832,9 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
             ntiles[sh] = n_objs * ((nb + lead + (1ull << sh) - 1) >> sh);
         const uint32_t tshift = c->tile_shift ? c->tile_shift : pick_tile_shift(ntiles);
         const uint64_t tpo = (nb + lead + (1ull << tshift) - 1) >> tshift;
-        StreamLock SL(c, s);
-        StreamState *S = SL.get();
+        std::unique_ptr<StreamLock> SL;
+        if (!held) SL.reset(new StreamLock(c, s));
+        StreamState *S = held ? held : SL->get();
         if (int r = tiles_reserve(S, n_objs * tpo, s)) return r;
         // the prefix's class from its exact length (pp: 4096 f_num / f_den = floor_len + rem / f_den)
         const int zc = pp.f_den == 0 || (pp.floor_len == 0 && pp.rem == 0) ? kZcNone
@@ -1035,9 +1050,26 @@ struct BatchScan {
     uint64_t ms = 0, blocks_s = 0, ntiles_s[kTileShiftMax + 1] = {};
     uint64_t first_off = 0, last_end = 0;
     bool dense_ok = true;
+    // uniform: every non-empty object has the first's size, dedup and ratio,
+    // at a constant stride (>= size) with entropy stepping by 2^32, i.e. the
+    // batch is a stream (s3dg_fill_controlled_stream's layout and seeds)
+    bool uni = true;
+    s3dg_obj_desc ufirst{}, ulast{};
+    uint64_t ustride = 0;
     int err = S3DG_OK;
     const char *msg = nullptr;
 };
+
+// Does object b continue the uniform run whose last object is a (stride 0: not yet known)?
+static inline bool uni_next(const s3dg_obj_desc &first, const s3dg_obj_desc &a, const s3dg_obj_desc &b,
+                           uint64_t &stride) {
+    if (b.size != first.size || b.dedup != first.dedup || b.f_num != first.f_num || b.f_den != first.f_den ||
+        b.entropy - a.entropy != (1ull << 32) || b.dst_off < a.dst_off)
+        return false;
+    const uint64_t st = b.dst_off - a.dst_off;
+    if (stride == 0) stride = st;
+    return st == stride && st >= first.size;
+}
 
 static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t k1, uintptr_t base, BatchScan &P,
                        s3dg_obj_desc *__restrict out, uint64_t split) {
@@ -1045,13 +1077,18 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
     // know that across the staging stores); the checks fold into one flag
     uint64_t m = 0, blocks = 0, zc_blocks[3] = {}, first = 0, last = 0, nt[kTileShiftMax + 1] = {};
     uint64_t ms = 0, blocks_s = 0, nts[kTileShiftMax + 1] = {};
-    bool dense = true, bad = false;
+    bool dense = true, bad = false, uni = true;
     uint32_t zc_num = 0, zc_den = 1;   // last compress seen and its zero_class
     int zc = kZcNone;
+    s3dg_obj_desc ufirst{}, uprev{};
+    uint64_t ustride = 0;
     for (uint64_t k = k0; k < k1; ++k) {
         const s3dg_obj_desc o = d[k];
         out[k - k0] = o;   // staged as is; empty objects are squeezed out afterwards (rare)
         if (o.size == 0) continue;
+        if (m == 0) ufirst = o;
+        else uni = uni && uni_next(ufirst, uprev, o, ustride);
+        uprev = o;
         const uint64_t nb = (o.size + kBlk - 1) / kBlk;
         bad |= (o.dst_off & 15u) != 0 || o.f_den == 0 || o.f_num >= o.f_den || nb >= (1ull << 31);
         const uint64_t x = nb + (((base + o.dst_off) >> 12) & 7);   // blocks behind the XCD lead
@@ -1093,6 +1130,10 @@ static void batch_scan(const s3dg_obj_desc *__restrict d, uint64_t k0, uint64_t 
     P.first_off = first;
     P.last_end = last;
     P.dense_ok = dense;
+    P.uni = uni;
+    P.ufirst = ufirst;
+    P.ulast = uprev;
+    P.ustride = ustride;
     for (uint32_t sh = kTileShiftMin; sh <= kTileShiftMax; ++sh) P.ntiles[sh] = nt[sh];
 }
 
@@ -1156,8 +1197,20 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             const BatchScan &Q = part[q];
             if (Q.err) return fail(Q.err, Q.msg);
             if (Q.m == 0) continue;
-            if (P.m == 0) P.first_off = Q.first_off;
-            else if (Q.first_off < P.last_end) P.dense_ok = false;
+            if (P.m == 0) {
+                P.first_off = Q.first_off;
+                P.ufirst = Q.ufirst;
+                P.uni = Q.uni;
+                P.ustride = Q.ustride;
+            } else {
+                if (Q.first_off < P.last_end) P.dense_ok = false;
+                // the runs join: Q's first object continues P's last, same stride
+                uint64_t st = P.ustride;
+                P.uni = P.uni && Q.uni && uni_next(P.ufirst, P.ulast, Q.ufirst, st) &&
+                        (Q.ustride == 0 || Q.ustride == st);
+                P.ustride = st;
+            }
+            P.ulast = Q.ulast;
             P.dense_ok = P.dense_ok && Q.dense_ok;
             P.last_end = Q.last_end;
             P.m += Q.m;
@@ -1170,6 +1223,20 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
         }
         const uint64_t m = P.m;
         if (m == 0) { k0 = k1; continue; }
+        // a uniform sub-batch is a stream: the stream paths (tiled records per
+        // 64 blocks, or the 2D kernel with no records at all) instead of a
+        // record per tile or granule (config 10's records
+        // were 6 % of its traffic).  Unless a batch layout is forced.
+        if (P.uni && m >= 2 && !c->tile_shift && !c->tile_force_dense) {
+            const uint64_t nb = (P.ufirst.size + kBlk - 1) / kBlk;
+            PrefixParams pp;
+            if (int r = make_prefix(nb, P.ufirst.dedup, P.ufirst.f_num, P.ufirst.f_den, &pp)) return r;
+            if (int r = fill_uniform(c, (uint8_t *)dst_base + P.ufirst.dst_off, P.ufirst.size, P.ustride, m, pp,
+                                     P.ufirst.entropy, 0, s, S))
+                return r;
+            k0 = k1;
+            continue;
+        }
         const uint64_t lead0 = ((base + P.first_off) >> 12) & 7;
         const uint64_t span = P.dense_ok ? lead0 + (P.last_end - P.first_off) / kBlk : 0;
         // layout: forced (s3dg_set_batch_tile) or least cost

@@ -27,6 +27,13 @@
 // memory itself); "staged" copies into a pinned bounce buffer of the staging
 // set and from there into the caller's buffer with host threads, overlapped
 // with the next chunk (DESIGN.md §5.8 has the A/B).
+// Registration (S3DLIO_HOST_REGISTER=1, opt-in): a pageable caller buffer
+// seen twice with the same address and length (the criterion loop of
+// benches/performance_microbenchmarks.rs:43-64 reuses one buffer) is
+// page-locked with hipHostRegister and from then on written by the kernel
+// directly, as library-pinned memory.  LIFETIME RULE: such a buffer must stay
+// allocated until s3dg_host_unregister(buf) (or NULL: all) or process exit;
+// freeing it while registered leaves the GPU mapping on the old pages.
 #include "s3dg_internal.h"
 #include "s3dlio_gpu.h"
 
@@ -433,27 +440,116 @@ int host_launch_blocks(HostStaging *sg, const HostJob &J, uint8_t *dst, uint64_t
     return S3DG_OK;
 }
 
+// ---- opt-in registration of repeated pageable buffers (S3DLIO_HOST_REGISTER=1)
+namespace {
+constexpr int kRegMax = 64;                        // registered ranges at once
+constexpr uint64_t kRegMaxBytes = 4ull << 30;      // registered bytes at once
+constexpr size_t kRegSeenMax = 256;                // remembered (address, length) sightings
+
+bool host_register_on() {
+    static const bool on = [] {
+        const char *v = getenv("S3DLIO_HOST_REGISTER");
+        return v && strcmp(v, "1") == 0;
+    }();
+    return on;
+}
+
+struct UserRegs {
+    std::mutex mu;
+    std::map<uintptr_t, std::pair<uint64_t, uint8_t *>> regs;   // page start -> (bytes, device pointer of start)
+    std::map<std::pair<uintptr_t, uint64_t>, int> seen;
+    uint64_t bytes = 0;
+};
+UserRegs &userregs() {
+    static UserRegs *r = new UserRegs();   // never freed: outlives static teardown
+    return *r;
+}
+
+// The device pointer of [p, p+n) when it lies in a registered range; on the
+// second call with this (p, n), registers its pages first.  nullptr: use the
+// regular paths.
+uint8_t *user_registered(const uint8_t *p, uint64_t n) {
+    UserRegs &R = userregs();
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(R.mu);
+    auto it = R.regs.upper_bound(a);
+    if (it != R.regs.begin()) {
+        --it;
+        if (a >= it->first && a + n <= it->first + it->second.first) return it->second.second + (a - it->first);
+    }
+    if (R.seen.size() >= kRegSeenMax) R.seen.clear();
+    if (++R.seen[{a, n}] < 2) return nullptr;
+    const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
+    if ((int)R.regs.size() >= kRegMax || R.bytes + (hi - lo) > kRegMaxBytes) return nullptr;
+    auto nx = R.regs.lower_bound(lo);                       // no overlap with a registered range
+    if (nx != R.regs.end() && nx->first < hi) return nullptr;
+    if (nx != R.regs.begin()) {
+        auto pv = std::prev(nx);
+        if (pv->first + pv->second.first > lo) return nullptr;
+    }
+    if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, (void *)lo, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        (void)hipHostUnregister((void *)lo);
+        return nullptr;
+    }
+    R.regs[lo] = {hi - lo, (uint8_t *)d};
+    R.bytes += hi - lo;
+    R.seen.erase({a, n});
+    return (uint8_t *)d + (a - lo);
+}
+}  // namespace
+
+extern "C" int s3dg_host_unregister(void *buf) {
+    UserRegs &R = userregs();
+    std::lock_guard<std::mutex> g(R.mu);
+    int released = 0;
+    for (auto it = R.regs.begin(); it != R.regs.end();) {
+        const uintptr_t a = (uintptr_t)buf;
+        if (!buf || (a >= it->first && a < it->first + it->second.first)) {
+            // kernels that wrote into it were waited for by the call that launched them
+            (void)hipHostUnregister((void *)it->first);
+            (void)hipGetLastError();
+            R.bytes -= it->second.first;
+            it = R.regs.erase(it);
+            ++released;
+        } else {
+            ++it;
+        }
+    }
+    R.seen.clear();
+    return released;
+}
+
 // The kernel may write the request's covering blocks straight into `buf`:
 // pinned memory this library allocated, 16-B aligned, and the blocks start
 // and end exactly at the request.
-static bool direct_target(const HostJob &J, const uint8_t *buf, uint64_t pos, uint64_t n) {
+static bool direct_geometry(const HostJob &J, const uint8_t *buf, uint64_t pos, uint64_t n) {
     const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
-    return n <= kDirectMax && aligned16(buf) && pos % unit == 0 && ((pos + n) % unit == 0 || pos + n == J.obj_len) &&
-           pinned_owned(buf, n);
+    return n <= kDirectMax && aligned16(buf) && pos % unit == 0 && ((pos + n) % unit == 0 || pos + n == J.obj_len);
+}
+
+static bool direct_target(const HostJob &J, const uint8_t *buf, uint64_t pos, uint64_t n) {
+    return direct_geometry(J, buf, pos, n) && pinned_owned(buf, n);
 }
 
 // A call without the copy engine: straight into the caller's buffer
 // (direct_target), or through the staging set's pinned bounce buffer in up
 // to kPiecesMax pieces on one stream, the calling thread copying piece k out
 // while pieces k+1.. are generated.
+// kdst: the device-visible address of buf (registered user memory), or buf.
 static int host_run_small(HostStaging *sg, Slot *S, const HostJob &J, uint8_t *buf, uint64_t pos, uint64_t n,
-                          bool direct) {
+                          bool direct, uint8_t *kdst) {
     if (int r = upload_user_base(sg, J)) return r;
     const uint64_t unit = J.dgen ? kDgenBlock : kBlk;
     const uint64_t b0 = pos / unit, b1 = (pos + n + unit - 1) / unit;
     hipStream_t st = sg->st[0];
     if (direct) {
-        if (int r = host_launch_blocks(sg, J, buf, b0, b1, st)) return r;
+        if (int r = host_launch_blocks(sg, J, kdst, b0, b1, st)) return r;
         H_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
         return S3DG_OK;
     }
@@ -549,8 +645,15 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     Slot *S = pool().slots[sg->slot];
     DeviceScope ds(S->device);
     H_TRY(ds.err, "hipSetDevice");
-    const bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
-    const int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct)
+    bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
+    uint8_t *kdst = buf;
+    if (!direct && !d2h_staged() && host_register_on() && direct_geometry(J, buf, pos, n)) {
+        if (uint8_t *d = user_registered(buf, n)) {   // a repeated pageable buffer, now page-locked
+            direct = true;
+            kdst = d;
+        }
+    }
+    const int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct, kdst)
                                                                 : host_run_chunks(sg, S, J, buf, pos, n);
     if (r != S3DG_OK)
         for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);   // nothing lands later

@@ -262,3 +262,38 @@ def test_small_calls_threads(L, oracle, golden_base):
     for t in ts:
         t.join()
     assert not errs, errs[0]
+
+
+def test_registered_pageable_buffer_child(oracle, golden_base):
+    """S3DLIO_HOST_REGISTER=1 (child process): a pageable buffer passed again
+    is page-locked and written by the kernel directly.
+    Every call's bytes equal the oracle's, guard pages around the buffer stay
+    untouched, s3dg_host_unregister reports the registration, and calls after
+    it (and with other lengths inside the buffer) are still exact."""
+    code = (
+        "import ctypes, hashlib, numpy as np, sys; sys.path.insert(0, %r)\n"
+        "from s3dlio_amd._lib import lib as L\n"
+        "from oracle import oracle_c as OC\n"
+        "gb = np.frombuffer(open(%r, 'rb').read(), np.uint8)\n"
+        "base = (ctypes.c_uint8 * 4096).from_buffer_copy(gb.tobytes())\n"
+        "MiB = 1 << 20; g = 8192\n"
+        "raw = np.full(3 * MiB + 2 * g + 4096, 0xA5, np.uint8)\n"
+        "o = (-raw.ctypes.data) %% 4096 + g\n"
+        "def run(size, d, c, ent):\n"
+        "    fn, fd = {1: (0, 1), 2: (1, 2), 3: (2, 3)}[c]\n"
+        "    assert L.s3dlio_fill_controlled_data_seeded(raw.ctypes.data + o, size, d, c, ent, base) == 0\n"
+        "    exp = OC.fill_controlled(size, d, fn, fd, ent, gb)\n"
+        "    assert bytes(raw[o:o + size]) == bytes(exp), (size, d, c, ent)\n"
+        "    assert (raw[o - g:o] == 0xA5).all() and (raw[o + 3 * MiB:] == 0xA5).all()\n"
+        "for k in range(5): run(MiB, 1, 1, 100 + k)\n"
+        "for k in range(3): run(2 * MiB + 4096, 2, 3, 200 + k)\n"
+        "run(MiB - 4096, 3, 2, 300)\n"
+        "n = L.s3dg_host_unregister(None); assert n >= 1, n\n"
+        "for k in range(3): run(3 * MiB, 1, 2, 400 + k)\n"
+        "assert L.s3dg_host_unregister(ctypes.c_void_p(raw.ctypes.data + o + 5)) == 1\n"
+        "assert L.s3dg_host_unregister(None) == 0\n"
+        "print('registered ok', n)\n" % (ROOT, os.path.join(ROOT, "tests", "golden", "base_block_ba5eb10c.bin")))
+    env = dict(os.environ, S3DLIO_HOST_REGISTER="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "registered ok" in out.stdout

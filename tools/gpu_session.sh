@@ -10,9 +10,12 @@
 #   file:PATH           pytest -m gpu on one test file
 #   smoke               __graft_entry__.smoke()
 #   bench:CFG[:ARGS]    bench.py --config CFG --steps 20 --warmup 5 ARGS (':'-separated)
+#   envbench:ENV:CFG    the same with ENV (comma-separated K=V) set
 #   driver              bench.py with no flags (the driver's own command)
 #   prof:CFG            rocprofv3 --kernel-trace --stats of bench.py --config CFG
 #   pmc:CFG:COUNTER     one rocprofv3 --pmc pass (WRITE_SIZE or FETCH_SIZE) of bench.py --config CFG
+#   rehearsal           bench.py N=8 (config 2) / N=4 (config 5, --d2h-full) launcher rehearsals on device 0
+#   soak[:N]            tests/test_gpu_fuzz.py with S3DG_FUZZ_SOAK=N (default 15)
 #   lab:SCRIPT[:ENV]    python tools/SCRIPT with ENV (comma-separated K=V) set
 # Environment: STEPS (bench steps, default 20), WARMUP (default 5).
 set -o pipefail
@@ -44,6 +47,11 @@ for step in "$@"; do
         timeout -k 10 400 python -u bench.py --config "$a" --steps "$STEPS" --warmup "$WARMUP" $extra \
             > "$OUT/$tag.log" 2>&1; rc=$?
         grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
+    envbench)
+        envs=$(echo "$a" | tr ',' ' ')
+        timeout -k 10 400 env $envs python -u bench.py --config "$b" --steps "$STEPS" --warmup "$WARMUP" \
+            > "$OUT/$tag.log" 2>&1; rc=$?
+        grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
     driver)
         timeout -k 10 400 python -u bench.py > "$OUT/$tag.log" 2>&1; rc=$?
         grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
@@ -56,6 +64,17 @@ for step in "$@"; do
         timeout -s KILL 240 rocprofv3 --pmc "$b" -d "$OUT/$tag" -o run --output-format csv \
             -- python3 bench.py --config "$a" --steps 3 --warmup 1 --no-ceiling --no-d2h --no-cpu-baseline \
             --no-verify > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -1 "$OUT/$tag.log";;
+    rehearsal)      # N=8 / N=4 launcher rehearsals, every rank on device 0 (not a scaling measurement)
+        timeout -k 10 300 python bench.py --gpus 8 --device-override 0 --objects 64 --config 2 --steps 3 \
+            --warmup 1 --no-ceiling > "$OUT/${tag}_n8_cfg2.log" 2>&1 && \
+        timeout -k 10 300 python bench.py --gpus 4 --device-override 0 --objects 400 --config 5 --steps 2 \
+            --warmup 1 --d2h-full --no-ceiling > "$OUT/${tag}_n4_cfg5_d2h_full.log" 2>&1; rc=$?
+        cat "$OUT/${tag}"_n*.log > "$OUT/$tag.log"
+        grep -h '^{' "$OUT/${tag}"_n*.log | cut -c1-300;;
+    soak)           # fuzz soak: SOAK x 26 seeded cases through every kernel and knob
+        S3DG_FUZZ_SOAK=${a:-15} timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -x -q \
+            --timeout 850 --timeout-method thread > "$OUT/$tag.log" 2>&1; rc=$?
         tail -1 "$OUT/$tag.log";;
     lab)
         envs=$(echo "$b" | tr ',' ' ')
