@@ -1520,14 +1520,16 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
         zlc.dyn_lds = occupancy_lds(c->zp_occ, 0);
         overlap = c->zp_overlap != 0;
     }
+    // the zero launch writes each block's first zw bytes (its zero prefix
+    // down to 16 B); the tail launch starts at draw z0 = zw / 8 and masks the
+    // rest of the prefix (at most 15 bytes, in its first store round)
     const uint64_t nchunks = (blk_hi - blk_lo) * n_objs;
-    const uint32_t zg = (uint32_t)(kDgenBlock * f_num / f_den / kBlk);
-    const bool zsplit = f_num > 0 && split && nchunks >= split && zg >= 8 &&
+    const uint32_t zw = (uint32_t)(kDgenBlock * f_num / f_den) & ~15u;
+    const bool zsplit = f_num > 0 && split && nchunks >= split && zw >= 8 * kBlk &&
                         (obj_size % kDgenBlock == 0 || blk_hi < nb);
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
-    if (int r = keystream_plan(c, 1, kDgenBlock, nchunks, f_num > 0 && !zsplit, A, &jt,
-                               zsplit ? (uint64_t)zg * (kBlk / 8) : 0))
+    if (int r = keystream_plan(c, 1, kDgenBlock, nchunks, f_num > 0 && !zsplit, A, &jt, zsplit ? zw / 8 : 0))
         return r;
     const uint64_t U = s3dg_unique_blocks(nb, dedup);
     A.cpo = blk_hi - blk_lo;
@@ -1554,7 +1556,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     hipStream_t s = (hipStream_t)stream;
     StreamState *SS = SL.get();
     if (zsplit && !overlap) {   // the prefixes' whole granules first (the tail launch masks a partial one)
-        HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zg, zlc, s),
+        HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zw, zlc, s),
                 "launch k_zero_prefix");
     } else if (zsplit) {        // on the side stream, concurrent with the tails (disjoint bytes)
         if (!SS->zs) HIP_TRY(hipStreamCreateWithFlags(&SS->zs, hipStreamNonBlocking), "hipStreamCreate(zero)");
@@ -1562,7 +1564,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
             if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
         HIP_TRY(hipEventRecord(SS->zfork, s), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(SS->zs, SS->zfork, 0), "hipStreamWaitEvent");
-        HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zg, zlc, SS->zs),
+        HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zw, zlc, SS->zs),
                 "launch k_zero_prefix");
         HIP_TRY(hipEventRecord(SS->zjoin, SS->zs), "hipEventRecord");
     }

@@ -466,27 +466,37 @@ UserRegs &userregs() {
 }
 
 // The device pointer of [p, p+n) when it lies in a registered range; on the
-// second call with this (p, n), registers its pages first.  nullptr: use the
+// second call with this (p, n), registers its pages first (may_register: the
+// call can take the direct path).  A range that overlaps registered ones
+// without lying inside one unregisters them first: HIP treats a copy into a
+// partly registered range as pinned and fails.  Host calls are synchronous,
+// so nothing is in flight on a range when it is dropped.  nullptr: use the
 // regular paths.
-uint8_t *user_registered(const uint8_t *p, uint64_t n) {
+uint8_t *user_registered(const uint8_t *p, uint64_t n, bool may_register) {
     UserRegs &R = userregs();
     const uintptr_t a = (uintptr_t)p;
     std::lock_guard<std::mutex> g(R.mu);
     auto it = R.regs.upper_bound(a);
     if (it != R.regs.begin()) {
         --it;
-        if (a >= it->first && a + n <= it->first + it->second.first) return it->second.second + (a - it->first);
+        if (a >= it->first && a + n <= it->first + it->second.first)
+            return may_register ? it->second.second + (a - it->first) : nullptr;
     }
+    const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
+    for (auto q = R.regs.begin(); q != R.regs.end();) {   // drop the registrations this range overlaps
+        if (q->first < hi && q->first + q->second.first > lo) {
+            (void)hipHostUnregister((void *)q->first);
+            (void)hipGetLastError();
+            R.bytes -= q->second.first;
+            q = R.regs.erase(q);
+        } else {
+            ++q;
+        }
+    }
+    if (!may_register) return nullptr;
     if (R.seen.size() >= kRegSeenMax) R.seen.clear();
     if (++R.seen[{a, n}] < 2) return nullptr;
-    const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
     if ((int)R.regs.size() >= kRegMax || R.bytes + (hi - lo) > kRegMaxBytes) return nullptr;
-    auto nx = R.regs.lower_bound(lo);                       // no overlap with a registered range
-    if (nx != R.regs.end() && nx->first < hi) return nullptr;
-    if (nx != R.regs.begin()) {
-        auto pv = std::prev(nx);
-        if (pv->first + pv->second.first > lo) return nullptr;
-    }
     if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
@@ -647,8 +657,9 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     H_TRY(ds.err, "hipSetDevice");
     bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
     uint8_t *kdst = buf;
-    if (!direct && !d2h_staged() && host_register_on() && direct_geometry(J, buf, pos, n)) {
-        if (uint8_t *d = user_registered(buf, n)) {   // a repeated pageable buffer, now page-locked
+    if (!direct && host_register_on()) {
+        const bool geo = !d2h_staged() && direct_geometry(J, buf, pos, n);
+        if (uint8_t *d = user_registered(buf, n, geo)) {   // a repeated pageable buffer, now page-locked
             direct = true;
             kdst = d;
         }

@@ -148,12 +148,12 @@ struct KeystreamArgs {
 };
 
 // DG1 zero prefixes in the fill's store shape (paired with a keystream launch
-// over the tails, A.z0 > 0): the first zg whole 4 KiB granules of each of
-// nchunks chunks (chunk c of object c / cpo at dst + (c / cpo)*obj_stride +
+// over the tails, A.z0 > 0): the first zw bytes (a multiple of 16) of each
+// of nchunks chunks (chunk c of object c / cpo at dst + (c / cpo)*obj_stride +
 // (c % cpo)*chunk_bytes) set to zero; one workgroup of 64 x lc.waves_per_block
-// threads per granule, lc.store, lc.dyn_lds capping the resident workgroups.
+// threads per 4 KiB granule, lc.store, lc.dyn_lds capping the resident workgroups.
 hipError_t launch_zero_prefix(uint8_t *dst, uint64_t nchunks, uint64_t cpo, uint64_t obj_stride, uint64_t chunk_bytes,
-                              uint32_t zg, const LaunchCfg &lc, hipStream_t s);
+                              uint32_t zw, const LaunchCfg &lc, hipStream_t s);
 
 // Per-stream queue counters of persistent keystream launches: 2 sets x 8
 // counters, 128 B apart (kKsCtrBytes, zeroed at allocation); `par` alternates

@@ -929,9 +929,10 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
 // fastdiv (m_cpo = floor(2^64 / cpo) + 1; y, cpo < 2^32).
 template <int SP, int NW>
 __global__ __launch_bounds__(64 * NW) void k_zero_prefix(uint8_t *dst, uint64_t y0, uint64_t cpo, uint64_t m_cpo,
-                                                         uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zg) {
+                                                         uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zw) {
     const uint32_t x = blockIdx.x;
-    if (x >= zg) return;
+    if ((uint64_t)x * kBlk >= zw) return;
+    const uint32_t lim = zw - x * kBlk;   // bytes of this granule below zw (a multiple of 16)
     const uint64_t y = y0 + blockIdx.y;
     const uint64_t ko = __umul64hi(m_cpo, y);
     const uint64_t cl = y - ko * cpo;
@@ -939,15 +940,21 @@ __global__ __launch_bounds__(64 * NW) void k_zero_prefix(uint8_t *dst, uint64_t 
     asm volatile("" : "+v"(off));   // the address on the VALU
     uint8_t *p = dst + off + threadIdx.x * 16;
     const u32x4 z = {0u, 0u, 0u, 0u};
+    if (lim >= kBlk) {
 #pragma unroll
-    for (int k = 0; k < 4 / NW; ++k) store16<SP>(p + k * 1024 * NW, z);
+        for (int k = 0; k < 4 / NW; ++k) store16<SP>(p + k * 1024 * NW, z);
+    } else {   // the partial last granule
+#pragma unroll
+        for (int k = 0; k < 4 / NW; ++k)
+            if (threadIdx.x * 16 + k * 1024 * NW < lim) store16<SP>(p + k * 1024 * NW, z);
+    }
 }
 
 template <int SP, int NW>
 void launch_zp_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *dst, uint64_t y0, uint64_t cpo, uint64_t m_cpo,
-                   uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zg) {
+                   uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zw) {
     hipLaunchKernelGGL((k_zero_prefix<SP, NW>), g, dim3(64 * NW), lds, s, dst, y0, cpo, m_cpo, obj_stride,
-                       chunk_bytes, zg);
+                       chunk_bytes, zw);
 }
 
 template <int D, int W>
@@ -1246,17 +1253,17 @@ hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu) {
 }
 
 hipError_t launch_zero_prefix(uint8_t *dst, uint64_t nchunks, uint64_t cpo, uint64_t obj_stride, uint64_t chunk_bytes,
-                              uint32_t zg, const LaunchCfg &lc, hipStream_t s) {
+                              uint32_t zw, const LaunchCfg &lc, hipStream_t s) {
     (void)hipGetLastError();
-    if (zg == 0 || nchunks == 0) return hipSuccess;
-    if (cpo == 0 || cpo > 0xFFFFFFFFull || nchunks > 0xFFFFFFFFull || (chunk_bytes & 4095u) ||
-        (uint64_t)zg * kBlk > chunk_bytes)
+    if (zw == 0 || nchunks == 0) return hipSuccess;
+    if (cpo == 0 || cpo > 0xFFFFFFFFull || nchunks > 0xFFFFFFFFull || (chunk_bytes & 4095u) || (zw & 15u) ||
+        zw > chunk_bytes)
         return hipErrorInvalidValue;
-    const uint32_t zgp = (zg + 7u) & ~7u;
+    const uint32_t zgp = ((zw + kBlk - 1) / kBlk + 7u) & ~7u;
     const uint64_t m_cpo = ~0ull / cpo + 1;
     for (uint64_t y0 = 0; y0 < nchunks; y0 += 65535) {
         const dim3 g(zgp, (uint32_t)((nchunks - y0) < 65535 ? (nchunks - y0) : 65535));
-        S3DG_DISPATCH(launch_zp_one, lc, g, lc.dyn_lds, s, dst, y0, cpo, m_cpo, obj_stride, chunk_bytes, zg);
+        S3DG_DISPATCH(launch_zp_one, lc, g, lc.dyn_lds, s, dst, y0, cpo, m_cpo, obj_stride, chunk_bytes, zw);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -45,7 +45,7 @@ def main():
     for rep in range(reps):
         for p in pts:
             kind, _, comp = p.partition("@")
-            comp = int(comp or 2)
+            comp = tuple(int(x) for x in comp.split("/")) if "/" in comp else int(comp or 2)
             order = names[rep % len(names):] + names[:rep % len(names)]
             if rep % 2:
                 order.reverse()

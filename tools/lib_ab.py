@@ -265,6 +265,9 @@ def main():
                 ms = [m for m, _, _ in per[(name, k)]]
                 mean_ms = sum(ms) / len(ms)
                 slow = [i for i, m in enumerate(ms) if m > thr]
+                # where the slow launches sit: (rep, position in its block, ms)
+                out["slow_launches"] = [(i // block, i % block, round(ms[i], 3)) for i in slow][:40]
+                out["slow_share_first_in_block"] = round(sum(1 for i in slow if i % block == 0) / len(ms), 4)
                 out.update({"GBps_mean": round(work[k.partition("@")[0]] / (mean_ms * 1e-3) / 1e9, 1),
                             "ms_mean": round(mean_ms, 4), "ms_p10": round(pct(ms, 0.1), 4),
                             "ms_p50": round(pct(ms, 0.5), 4), "ms_p90": round(pct(ms, 0.9), 4),
