@@ -445,9 +445,12 @@ def main() -> int:
                                                "groups of 16; a persistent grid over per-XCD unit queues from 6 "
                                                "rounds of resident waves up")
     elif kind in ("dgen", "dgen_stream"):
-        kernel, launch_shape = "k_keystream (DG1 mode)", (
-            ("k_keystream<64,4>: 512 draws per lane, 256 lanes per 1 MiB DG1 block, zero-prefix waves skip "
-             "the PRNG, XCD groups of 32 waves" if fn else
+        kernel, launch_shape = ("k_zero_prefix + k_keystream (DG1 tails)" if fn else "k_keystream (DG1 mode)"), (
+            ("k_zero_prefix: each 1 MiB DG1 block's whole 4 KiB granules of zeros in the fill's store shape "
+             "(prefixes on a 64-B line: 4-wave workgroups, 5 per CU, nt sc1, before the tails; mid-line: 1-wave, "
+             "14 per CU, on a side stream beside them), then k_keystream<64,1> over the blocks' tails (64 lanes "
+             "per tail, jump state sequence on the scalar unit, the rest of the prefix zeroed in the lane rows)"
+             if fn else
              "k_keystream<64,1>: 2048 draws per lane, 64 lanes per 1 MiB DG1 block, jump state sequence on the "
              "scalar unit, XCD groups of 16 waves, a persistent grid over per-XCD unit queues from 6 rounds of "
              "resident waves up")

@@ -144,7 +144,10 @@ int s3dg_set_keystream_persist(s3dg_ctx *ctx, int rounds);
  * `waves` per 4 KiB workgroup (1, 2, 4), `occupancy` resident workgroups per
  * CU cap (0 = none), `store` policy (as s3dg_set_store_policy), `overlap` 1 =
  * on a side stream concurrent with the tails (the caller's stream waits for
- * both); negative = default for each.  A tuning knob; results are identical. */
+ * both); negative = default for each (measured per prefix class: prefixes
+ * ending on a 64-B line, e.g. compress 2 or 4: 4 waves, 5 per CU, nt sc1, in
+ * order; others: 1 wave, 14 per CU, nt sc1, overlapped).  A tuning knob;
+ * results are identical. */
 int s3dg_set_dgen_zero_split(s3dg_ctx *ctx, int chunks, int waves, int occupancy, int store, int overlap);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
 /* Resident workgroups per CU the current settings give (HIP occupancy API):

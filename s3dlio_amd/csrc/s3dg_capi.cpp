@@ -144,10 +144,17 @@ constexpr int kDgenPrefixWaves = 4, kDgenPrefixXcdWaves = 32;
 // prefixes as whole 4 KiB granules in the fill's store shape (k_zero_prefix),
 // then the keystream over the tails alone (s3dg_set_dgen_zero_split;
 // DESIGN.md §5.3).  The zero launch's occupancy cap and store policy.
+// The zero launch's shape per prefix class, measured (tools/dg1_split_lab.py,
+// profiles/r05/i, j: ten 8 GiB DG1 objects, one launch each / all in one):
+// prefixes that end on a 64-B line (c = 2, 4, ...): 4-wave workgroups, 5
+// resident per CU, nt sc1 stores, after the tails' launch on the same stream
+// (c2 0.843 / 0.854, c4 0.875 against one keystream launch's 0.781 / 0.848,
+// 0.842); mid-line prefixes (c = 3, 1.5, ...): 1-wave workgroups, 14 per CU,
+// nt sc1, on a side stream concurrent with the tails (c3 0.794 / 0.866, c1.5
+// 0.857 against 0.735 / 0.779, 0.729).  Index: [0] line-aligned, [1] mid-line.
 constexpr uint64_t kDefaultDgenZeroSplit = 64;
-constexpr int kDefaultZeroPrefixWaves = 1, kDefaultZeroPrefixOcc = 0;
-constexpr int kDefaultZeroPrefixStore = kStoreSC1;
-constexpr int kDefaultZeroPrefixOverlap = 0;   // 1: the zero launch on a side stream, concurrent with the tails
+constexpr int kZeroPrefixWaves[2] = {4, 1}, kZeroPrefixOcc[2] = {5, 14};
+constexpr int kZeroPrefixStore[2] = {kStoreNTSC1, kStoreNTSC1}, kZeroPrefixOverlap[2] = {0, 1};
 
 // Launch state private to one stream: the tile-record map of tiled launches
 // and the batch-descriptor staging.  Launches on one stream are ordered by
@@ -212,8 +219,7 @@ struct s3dg_ctx {
     bool ks_auto_waves[2] = {true, true}, ks_auto_xcd[2] = {true, true};          // not set by the caller
     int ks_persist = -1;               // persistent keystream launches from this many rounds (-1: default)
     uint64_t dgen_zero_split = kDefaultDgenZeroSplit;   // DG1 zero prefix + tail launches from this many blocks
-    int zp_waves = kDefaultZeroPrefixWaves, zp_occ = kDefaultZeroPrefixOcc, zp_store = kDefaultZeroPrefixStore;
-    int zp_overlap = kDefaultZeroPrefixOverlap;
+    int zp_waves = -1, zp_occ = -1, zp_store = -1, zp_overlap = -1;   // -1: per prefix class (kZeroPrefix*)
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // tile maps and batch staging, one set per stream (s3dg::StreamState)
@@ -737,10 +743,10 @@ int s3dg_set_dgen_zero_split(s3dg_ctx *c, int chunks, int waves, int occupancy, 
     if (store > kStoreNTSC1) return fail(S3DG_EINVAL, "store policy must be 0, 1, 2, 3 or negative");
     std::lock_guard<std::mutex> g(c->mu);
     c->dgen_zero_split = chunks < 0 ? kDefaultDgenZeroSplit : (uint64_t)chunks;
-    c->zp_waves = waves <= 0 ? kDefaultZeroPrefixWaves : waves;
-    c->zp_occ = occupancy < 0 ? kDefaultZeroPrefixOcc : occupancy;
-    c->zp_store = store < 0 ? kDefaultZeroPrefixStore : store;
-    c->zp_overlap = overlap < 0 ? kDefaultZeroPrefixOverlap : (overlap ? 1 : 0);
+    c->zp_waves = waves <= 0 ? -1 : waves;
+    c->zp_occ = occupancy < 0 ? -1 : occupancy;
+    c->zp_store = store < 0 ? -1 : store;
+    c->zp_overlap = overlap < 0 ? -1 : (overlap ? 1 : 0);
     return S3DG_OK;
 }
 
@@ -1513,18 +1519,21 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     LaunchCfg zlc;
     bool overlap;
     {
+        const int k = (kDgenBlock * f_num) % f_den == 0 && (kDgenBlock * f_num / f_den) % 64 == 0 ? 0 : 1;
         std::lock_guard<std::mutex> g(c->mu);
         split = c->dgen_zero_split;
-        zlc.store = c->zp_store;
-        zlc.waves_per_block = c->zp_waves;
-        zlc.dyn_lds = occupancy_lds(c->zp_occ, 0);
-        overlap = c->zp_overlap != 0;
+        zlc.store = c->zp_store >= 0 ? c->zp_store : kZeroPrefixStore[k];
+        zlc.waves_per_block = c->zp_waves > 0 ? c->zp_waves : kZeroPrefixWaves[k];
+        zlc.dyn_lds = occupancy_lds(c->zp_occ >= 0 ? c->zp_occ : kZeroPrefixOcc[k], 0);
+        overlap = (c->zp_overlap >= 0 ? c->zp_overlap : kZeroPrefixOverlap[k]) != 0;
     }
-    // the zero launch writes each block's first zw bytes (its zero prefix
-    // down to 16 B); the tail launch starts at draw z0 = zw / 8 and masks the
-    // rest of the prefix (at most 15 bytes, in its first store round)
+    // the zero launch writes each block's whole 4 KiB granules of zeros (zw
+    // bytes); the tail launch starts at draw z0 = zw / 8 and zeroes the rest
+    // of the prefix (< 4 KiB) in its lane rows.  Tails that start inside a
+    // granule (zw down to 16 B) ran 25-35 % slower: lane regions off the
+    // 128-B lines (profiles/r05/g).
     const uint64_t nchunks = (blk_hi - blk_lo) * n_objs;
-    const uint32_t zw = (uint32_t)(kDgenBlock * f_num / f_den) & ~15u;
+    const uint32_t zw = (uint32_t)(kDgenBlock * f_num / f_den) & ~(kBlk - 1);
     const bool zsplit = f_num > 0 && split && nchunks >= split && zw >= 8 * kBlk &&
                         (obj_size % kDgenBlock == 0 || blk_hi < nb);
     KeystreamArgs A{};

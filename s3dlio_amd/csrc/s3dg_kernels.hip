@@ -773,19 +773,19 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
 #endif
     row_dest();
 
-    // Wave-uniform fast paths: a D-draw group needs no masking when no lane
-    // of the wave is inside a zero prefix or at its chunk's 1-4 byte tail;
-    // the stores need no guards when every region of the wave is full length.
-    // Per lane: iterations < it_plain may touch the zero prefix (draws below
-    // ceil(zlen/8)); iteration it_tail holds the 1-4 byte tail draw.
-    const uint64_t zdraws = (zlen + 7) >> 3;
-    const uint64_t zi = zdraws > d0 ? (zdraws - d0 + D - 1) / D : 0;
-    const uint32_t it_plain = zi < iters ? (uint32_t)zi : iters;
+    // Wave-uniform fast path: a D-draw group is generated unmasked unless a
+    // lane of the wave is at its chunk's 1-4 byte tail (iteration it_tail);
+    // bytes inside a zero prefix are then zeroed in the lane's LDS row by the
+    // lanes concerned alone (round 5: the whole wave used to take the masked
+    // path while any lane touched the prefix, e.g. 6 of 8 store rounds of a
+    // DG1 c3 wave, or 8 of 11 of a tail launch's waves, profiles/r05/).  The
+    // stores need no guards when every region of the wave is full length.
     const uint32_t it_tail = (tail_hi && tail_draw >= d0 && tail_draw < d0 + span)
                                  ? (uint32_t)((tail_draw - d0) / D) : 0xFFFFFFFFu;
     for (uint32_t it = 0; it < iters; ++it) {
         const uint64_t dg = d0 + (uint64_t)it * D;
-        if (__all(it >= it_plain && it != it_tail)) {
+        const bool plain = __all(it != it_tail);
+        if (plain) {
 #pragma unroll
             for (int q = 0; q < D; q += 2) {
 #if S3DG_ABLATE & 32
@@ -809,6 +809,23 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
                 if (8 * d + 8 < zlen) rbv &= (8 * d + 16 <= zlen) ? 0ull : (~0ull << (8 * (zlen - 8 * d - 8)));
                 *reinterpret_cast<u32x4 *>(myrows + l * RS + q * 8) =
                     u32x4{(uint32_t)ra, (uint32_t)(ra >> 32), (uint32_t)rbv, (uint32_t)(rbv >> 32)};
+            }
+        }
+        // zero-prefix bytes of this row (fast path only: the masked path zeroed them)
+        const uint64_t row0 = 8 * dg;
+        if (plain && row0 < zlen) {
+            const uint32_t zb = (zlen - row0) < (uint64_t)(D * 8) ? (uint32_t)(zlen - row0) : (uint32_t)(D * 8);
+            uint8_t *row = myrows + l * RS;
+            for (uint32_t p = 0; p + 16 <= zb; p += 16) *reinterpret_cast<u32x4 *>(row + p) = u32x4{0u, 0u, 0u, 0u};
+            if (zb & 15u) {
+                u32x4 *pc = reinterpret_cast<u32x4 *>(row + (zb & ~15u));
+                u32x4 v = *pc;
+                const uint32_t nz = zb & 15u;   // leading bytes to zero
+                v.x = nz >= 4 ? 0u : v.x & (~0u << (8 * nz));
+                v.y = nz >= 8 ? 0u : nz <= 4 ? v.y : v.y & (~0u << (8 * (nz - 4)));
+                v.z = nz >= 12 ? 0u : nz <= 8 ? v.z : v.z & (~0u << (8 * (nz - 8)));
+                v.w = nz <= 12 ? v.w : v.w & (~0u << (8 * (nz - 12)));
+                *pc = v;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

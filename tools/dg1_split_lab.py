@@ -7,7 +7,7 @@ s3dg_dgen_fill each) or 17 (the ten in one s3dg_dgen_fill_stream launch) at
 the given compress, timed with HIP events; mean GB/s over the samples.
 
     python tools/dg1_split_lab.py          # GPU box
-LAB_SETTINGS: "name=chunks/waves/occ/store/overlap;..." (default below), LAB_POINTS:
+LAB_SETTINGS: "name=chunks/waves/occ/store/overlap[/xcd_group[/lane_draws]];..." (default below), LAB_POINTS:
 "cfg15@2;cfg17@2;cfg15@3" (@compress), LAB_REPS (default 6).
 Tooling only: nothing in the product imports this."""
 import json, os, statistics, sys
@@ -25,9 +25,14 @@ def main():
     sets = {}
     for item in os.environ.get("LAB_SETTINGS", DEFAULT).split(";"):
         name, _, spec = item.partition("=")
-        ch, w, occ, st, ov = (int(x) for x in spec.split("/"))
+        f = [int(x) for x in spec.split("/")]
+        ch, w, occ, st, ov = f[:5]
         c = S.Context(0, base_seed=S.DEFAULT_BASE_SEED)
         c.set_dgen_zero_split(ch, w, occ, st, ov)
+        if len(f) > 5 and f[5]:          # DG1 keystream XCD group (waves) for the tails
+            c.set_keystream_xcd_group(1, f[5])
+        if len(f) > 6 and f[6]:          # DG1 keystream draws per lane (tails: lanes of a 64-lane wave)
+            c.set_keystream_shape(1, 0, 0, 0, f[6], -1)
         sets[name] = c
     pts = os.environ.get("LAB_POINTS", "cfg15@2;cfg17@2;cfg15@3;cfg17@3").split(";")
     reps = int(os.environ.get("LAB_REPS", "6"))
