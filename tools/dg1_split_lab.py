@@ -2,9 +2,10 @@
 """DG1 with a zero prefix: one keystream launch vs the zero-prefix + tail
 split (s3dg_set_dgen_zero_split), and the zero launch's occupancy cap and
 store policy.  One context per setting, interleaved, order rotated per rep;
-each sample one step of bench.py's configs 15 (ten 8 GiB objects, one
-s3dg_dgen_fill each) or 17 (the ten in one s3dg_dgen_fill_stream launch) at
-the given compress, timed with HIP events; mean GB/s over the samples.
+each sample one step of bench.py's configs 14/15 (ten 8 GiB objects, one
+s3dg_dgen_fill each; dedup 1/2) or 16/17 (the ten in one
+s3dg_dgen_fill_stream launch) at the given compress (default 1 for 14/16, 2
+for 15/17), timed with HIP events; mean GB/s over the samples.
 
     python tools/dg1_split_lab.py          # GPU box
 LAB_SETTINGS: "name=chunks/waves/occ/store/overlap[/xcd_group[/lane_draws]];..." (default below), LAB_POINTS:
@@ -40,17 +41,19 @@ def main():
     G8 = 8 * GiB
 
     def run(c, kind, comp):
-        if kind == "cfg15":
+        d = 2 if kind in ("cfg15", "cfg17") else 1          # configs 14 / 16: dedup 1
+        if kind in ("cfg14", "cfg15"):                      # one launch per 8 GiB object
             for t in range(10):
-                c.dgen_fill(buf[t * G8:(t + 1) * G8], G8, dedup=2, compress=comp, seed=0x5EED + t)
-        else:
-            c.dgen_fill_stream(buf, G8, 10, dedup=2, compress=comp, seed_base=0x5EED)
+                c.dgen_fill(buf[t * G8:(t + 1) * G8], G8, dedup=d, compress=comp, seed=0x5EED + t)
+        else:                                               # the ten in one launch
+            c.dgen_fill_stream(buf, G8, 10, dedup=d, compress=comp, seed_base=0x5EED)
     res, digest = {}, {}
     names = list(sets)
     for rep in range(reps):
         for p in pts:
             kind, _, comp = p.partition("@")
-            comp = tuple(int(x) for x in comp.split("/")) if "/" in comp else int(comp or 2)
+            comp = (tuple(int(x) for x in comp.split("/")) if "/" in comp
+                    else int(comp or (1 if kind in ("cfg14", "cfg16") else 2)))
             order = names[rep % len(names):] + names[:rep % len(names)]
             if rep % 2:
                 order.reverse()

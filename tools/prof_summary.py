@@ -22,8 +22,8 @@ import csv, json, os, shutil, subprocess, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-STEP_KERNELS = ("k_fill_stream", "k_fill_batch", "k_keystream", "k_tile_map_uniform", "k_batch_map")
-FILL_KERNELS = ("k_fill_stream", "k_fill_batch", "k_keystream")
+STEP_KERNELS = ("k_fill_stream", "k_fill_batch", "k_keystream", "k_zero_prefix", "k_tile_map_uniform", "k_batch_map")
+FILL_KERNELS = ("k_fill_stream", "k_fill_batch", "k_keystream", "k_zero_prefix")
 
 
 def bench_line(path):
