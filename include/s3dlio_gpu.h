@@ -90,7 +90,8 @@ int s3dg_set_occupancy(s3dg_ctx *ctx, int stream_wgs_per_cu, int batch_wgs_per_c
  * block wait until `ticks` wall-clock ticks (10 ns) after its workgroup
  * started; 0 = no floor, negative = per launch (100 when most of the
  * launch's blocks have a zero prefix of at least half the block that ends
- * inside a 64-B line, e.g. compress 3; none otherwise).  Measured on MI355X;
+ * inside a 64-B line, e.g. compress 3, and for uniform streams of objects of
+ * >= 2 MiB without a zero prefix; none otherwise).  Measured on MI355X;
  * results are identical. */
 int s3dg_set_batch_pace(s3dg_ctx *ctx, int ticks);
 /* Batch launches: distance (in units of 64 blocks) at which workgroups warm

@@ -60,6 +60,16 @@ constexpr int kDefaultBatchRtFloor = -1;   // per launch
 // (DESIGN.md §5.1); 0 = off.
 constexpr uint32_t kDefaultSplitBlocks = 0;
 constexpr uint32_t kRtFloorMidZeros = 100;
+// Uniform streams of large objects without a zero prefix (config 2): the same
+// 1 us store floor.  On some boxes 10-45 % of such launches run 12.1-12.9 ms
+// instead of 11.0-11.2 (round 4's driver line; round 5's final and lab boxes,
+// at the normal clock and power): with the floor those boxes ran 0 % and
+// 0-30 % slow launches, +1.0 / +1.9 % by mean (tools/dip_lab.py, bench.py
+// --pace A/Bs, profiles/r05/dip/), while a box without them lost 0.2 %.
+// Small objects (config 8) and batches (config 4) showed few slow launches
+// and no gain (0 / -0.7 %), so they keep no floor.  DESIGN.md §5.1.4.
+constexpr uint32_t kRtFloorLargeUniform = 100;
+constexpr uint64_t kRtFloorLargeBlocks = 512;   // objects of >= 2 MiB
 // Launch classes by zero prefix (per launch; batches by majority of blocks)
 enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
 // The mid-line class's store floor is checked by measurement (round 4).  It
@@ -851,8 +861,9 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
         ZcTuner::Pending probe{};
         const int cand = tune_pick(c, zc, obj_size * n_objs, &timed, &probe);
         if (timed) tune_mark(c, zc, probe, false, s);
-        const hipError_t le = launch_fill_uniform_tiles(cfg_for(c, true, cand ? kZcNone : zc), dst, obj_size, stride,
-                                                        n_objs, (uint32_t)tpo, tshift, lead,
+        LaunchCfg lc = cfg_for(c, true, cand ? kZcNone : zc);
+        if (zc == kZcNone && c->batch_rt_floor < 0 && nb >= kRtFloorLargeBlocks) lc.rt_floor = kRtFloorLargeUniform;
+        const hipError_t le = launch_fill_uniform_tiles(lc, dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift, lead,
                                                         seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s);
         if (timed) tune_mark(c, zc, probe, true, s);
         HIP_TRY(le,
