@@ -150,6 +150,12 @@ int s3dg_set_keystream_persist(s3dg_ctx *ctx, int rounds);
  * order; others: 1 wave, 14 per CU, nt sc1, overlapped).  A tuning knob;
  * results are identical. */
 int s3dg_set_dgen_zero_split(s3dg_ctx *ctx, int chunks, int waves, int occupancy, int store, int overlap);
+/* One-object DG1 launches that run a persistent grid (see above): their last
+ * `chunks` 1 MiB blocks in lanes of half the length, handed out after the
+ * others, so the launch drains on shorter units.  0 = off; negative =
+ * default (half a resident round of units).  A tuning knob; results are
+ * identical. */
+int s3dg_set_keystream_tail(s3dg_ctx *ctx, int chunks);
 int s3dg_query_keystream_occupancy(s3dg_ctx *ctx, int mode, int *wgs_per_cu);
 /* Resident workgroups per CU the current settings give (HIP occupancy API):
  * batch 0 = stream launches, 1 = batch launches, 2 = batch launches whose

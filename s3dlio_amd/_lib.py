@@ -69,6 +69,7 @@ SIGNATURES = {
     "s3dg_set_keystream_shape": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_u64, c_int]),
     "s3dg_set_keystream_xcd_group": (c_int, [c_vp, c_int, c_u32]),
     "s3dg_set_keystream_persist": (c_int, [c_vp, c_int]),
+    "s3dg_set_keystream_tail": (c_int, [c_vp, c_int]),
     "s3dg_set_dgen_zero_split": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int]),
     "s3dg_query_keystream_occupancy": (c_int, [c_vp, c_int, ctypes.POINTER(c_int)]),
     "s3dg_unique_blocks": (c_u64, [c_u64, c_u64]),

@@ -230,6 +230,7 @@ struct s3dg_ctx {
     int ks_persist = -1;               // persistent keystream launches from this many rounds (-1: default)
     uint64_t dgen_zero_split = kDefaultDgenZeroSplit;   // DG1 zero prefix + tail launches from this many blocks
     int zp_waves = -1, zp_occ = -1, zp_store = -1, zp_overlap = -1;   // -1: per prefix class (kZeroPrefix*)
+    int64_t ks_tail = -1;              // one-object DG1 launches: chunks in half-length lanes at the end (-1: auto)
     void *base_dev = nullptr;          // 4 KiB base block in HBM
     uint8_t base_host[kBlk];
     // tile maps and batch staging, one set per stream (s3dg::StreamState)
@@ -757,6 +758,13 @@ int s3dg_set_dgen_zero_split(s3dg_ctx *c, int chunks, int waves, int occupancy, 
     c->zp_occ = occupancy < 0 ? -1 : occupancy;
     c->zp_store = store < 0 ? -1 : store;
     c->zp_overlap = overlap < 0 ? -1 : (overlap ? 1 : 0);
+    return S3DG_OK;
+}
+
+int s3dg_set_keystream_tail(s3dg_ctx *c, int chunks) {
+    if (!c) return fail(S3DG_EINVAL, "null context");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->ks_tail = chunks < 0 ? -1 : chunks;
     return S3DG_OK;
 }
 
@@ -1397,6 +1405,26 @@ int s3dg_xoshiro_jump(uint64_t *state4, uint64_t n) {
 }
 
 // lanes per chunk + draws per lane for a chunk size; jump table cached per ctx
+// The device jump table of lanes sub < lpc starting at draws z0 + sub*span
+// (cached per context): jtab[sub] = x^(z0 + sub*span) mod P.
+static int jump_table(s3dg_ctx *c, uint32_t lpc, uint64_t span, uint64_t z0, const uint64_t **jtab) {
+    std::lock_guard<std::mutex> g(c->mu);
+    const std::pair<uint64_t, uint64_t> key{((uint64_t)lpc << 32) | span, z0};
+    auto it = c->jtabs.find(key);
+    if (it == c->jtabs.end()) {
+        std::vector<uint64_t> h(4 * (size_t)lpc, 0);
+        for (uint32_t k = 0; k < lpc; ++k)
+            if (!jump_poly(z0 + (uint64_t)k * span, &h[4 * k]))
+                return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
+        uint64_t *d = nullptr;
+        HIP_TRY(hipMalloc(&d, h.size() * 8), "hipMalloc(jump table)");
+        HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(jump table)");
+        it = c->jtabs.emplace(key, d).first;
+    }
+    *jtab = it->second;
+    return S3DG_OK;
+}
+
 // z0 > 0: the lanes cover draws [z0, chunk_bytes / 8) of every chunk (the
 // tails of a DG1 zero-prefix split), one wave per tail when it has >= 64 x 256 draws.
 static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t nchunks, bool zero_prefix,
@@ -1428,21 +1456,7 @@ static int keystream_plan(s3dg_ctx *c, int mode, uint64_t chunk_bytes, uint64_t 
     A.lpc = lpc;
     A.span = (uint32_t)span;
     A.z0 = z0;
-    std::lock_guard<std::mutex> g(c->mu);
-    const std::pair<uint64_t, uint64_t> key{((uint64_t)lpc << 32) | span, z0};
-    auto it = c->jtabs.find(key);
-    if (it == c->jtabs.end()) {
-        std::vector<uint64_t> h(4 * (size_t)lpc, 0);
-        for (uint32_t k = 0; k < lpc; ++k)
-            if (!jump_poly(z0 + (uint64_t)k * span, &h[4 * k]))
-                return fail(S3DG_EINVAL, "xoshiro characteristic polynomial unavailable");
-        uint64_t *d = nullptr;
-        HIP_TRY(hipMalloc(&d, h.size() * 8), "hipMalloc(jump table)");
-        HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(jump table)");
-        it = c->jtabs.emplace(key, d).first;
-    }
-    *jtab = it->second;
-    return S3DG_OK;
+    return jump_table(c, lpc, span, z0, jtab);
 }
 
 // The stream's queue counters for persistent keystream launches, allocated
@@ -1545,8 +1559,17 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     // 128-B lines (profiles/r05/g).
     const uint64_t nchunks = (blk_hi - blk_lo) * n_objs;
     const uint32_t zw = (uint32_t)(kDgenBlock * f_num / f_den) & ~(kBlk - 1);
-    const bool zsplit = f_num > 0 && split && nchunks >= split && zw >= 8 * kBlk &&
-                        (obj_size % kDgenBlock == 0 || blk_hi < nb);
+    const bool ragged_end = obj_size % kDgenBlock != 0 && blk_hi == nb;
+    if (f_num > 0 && split && ragged_end && blk_hi - 1 > blk_lo && (blk_hi - 1 - blk_lo) * n_objs >= split &&
+        zw >= 8 * kBlk) {
+        // the objects' full blocks split, their short last blocks in a launch of their own
+        if (int r = s3dg_internal_dgen_chunk(c, dst, obj_size, stride, n_objs, blk_lo, blk_hi - 1, dedup, f_num, f_den,
+                                             seed_base, first_obj, stream))
+            return r;
+        return s3dg_internal_dgen_chunk(c, (uint8_t *)dst + (blk_hi - 1 - blk_lo) * kDgenBlock, obj_size, stride,
+                                        n_objs, blk_hi - 1, blk_hi, dedup, f_num, f_den, seed_base, first_obj, stream);
+    }
+    const bool zsplit = f_num > 0 && split && nchunks >= split && zw >= 8 * kBlk && !ragged_end;
     KeystreamArgs A{};
     const uint64_t *jt = nullptr;
     if (int r = keystream_plan(c, 1, kDgenBlock, nchunks, f_num > 0 && !zsplit, A, &jt, zsplit ? zw / 8 : 0))
@@ -1588,7 +1611,42 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
                 "launch k_zero_prefix");
         HIP_TRY(hipEventRecord(SS->zjoin, SS->zs), "hipEventRecord");
     }
-    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, s, kc, c->cus, c->ks_persist), "launch k_keystream(dgen)");
+    // One object: its last T chunks in lanes of half the length, handed out
+    // after the others by a persistent launch, so the launch drains on units
+    // half as long (default T: half a resident round of 1-wave units, i.e. one
+    // round of half units).
+    KeystreamArgs A2{};
+    const uint64_t *jt2 = nullptr;
+    bool tail = false;
+    int64_t tail_chunks;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        tail_chunks = c->ks_tail;
+    }
+    if (tail_chunks < 0) {
+        int res = 0;
+        if (keystream_occupancy(sh, &res) != hipSuccess) res = 0;
+        (void)hipGetLastError();
+        tail_chunks = (int64_t)((uint64_t)res * (uint64_t)c->cus * (uint64_t)sh.waves * 64 / A.lpc / 2);
+    }
+    const uint32_t span2 = A.span / 2;
+    if (n_objs == 1 && tail_chunks > 0 && sh.waves == 1 && A.lpc >= 64 && A.lpc <= 512 && span2 >= kKsMinSpan &&
+        span2 % (uint32_t)sh.draws == 0 && nchunks >= 8 * (uint64_t)tail_chunks) {
+        const uint64_t T = (uint64_t)tail_chunks;
+        A2 = A;
+        A2.lpc = 2 * A.lpc;
+        A2.span = span2;
+        A2.nchunks = T;
+        A2.cpo = T;
+        A2.chunk0 = A.chunk0 + (nchunks - T);
+        A2.doff = (nchunks - T) * kDgenBlock;
+        A.nchunks = nchunks - T;
+        A.cpo = nchunks - T;
+        if (int r = jump_table(c, A2.lpc, A2.span, A2.z0, &jt2)) return r;
+        tail = true;
+    }
+    HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, s, kc, c->cus, c->ks_persist, tail ? &A2 : nullptr, jt2),
+            "launch k_keystream(dgen)");
     if (zsplit && overlap) HIP_TRY(hipStreamWaitEvent(s, SS->zjoin, 0), "hipStreamWaitEvent");
     return S3DG_OK;
 }

@@ -145,6 +145,9 @@ struct KeystreamArgs {
     // z0 + sub*span; jtab[sub] = x^(z0 + sub*span)): a DG1 launch over the
     // chunks' tails whose zero prefixes k_zero_prefix has written
     uint64_t z0;
+    // byte offset of this argument set's first chunk from the kernel's dst
+    // (the tail set of a persistent launch, below)
+    uint64_t doff;
 };
 
 // DG1 zero prefixes in the fill's store shape (paired with a keystream launch
@@ -176,9 +179,13 @@ struct KsShape {
 // static grid.  cus: compute units of the device.  persist_rounds: launches
 // of at least that many rounds of resident waves run persistent (0: never;
 // negative: the default rule, 1-wave workgroups from kKsPersistRounds).
+// tail / tail_jtab: a second argument set (other lanes per chunk, A2.doff)
+// whose units a persistent launch hands out after A's, so the launch ends on
+// shorter units; a static-grid launch runs it as a second launch.
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab,
                            const KsShape &sh, hipStream_t s, KsCounters *ctrs = nullptr, int cus = 0,
-                           int persist_rounds = -1);
+                           int persist_rounds = -1, const KeystreamArgs *tail = nullptr,
+                           const uint64_t *tail_jtab = nullptr);
 hipError_t keystream_occupancy(const KsShape &sh, int *wgs_per_cu);
 
 // thr/nthr: records for the tiled shape's trailing loads (lc.prefetch_tiles), or null

@@ -661,7 +661,7 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
     const uint64_t cl = c - ko * cpo;
     const uint64_t cg = A.chunk0 + cl;                               // chunk index in the object
     const uint32_t sub = (uint32_t)(gl & (lpc - 1));
-    const uint64_t coff = ko * A.obj_stride + cl * A.chunk_bytes;    // offset within dst
+    const uint64_t coff = A.doff + ko * A.obj_stride + cl * A.chunk_bytes;   // offset within dst
     const uint64_t seed_base = A.seed_base + ko * A.seed_step;
     const uint64_t gofs = cg * A.chunk_bytes;                        // offset within the object
     const uint64_t clen = (c < A.nchunks && gofs < A.obj_len)
@@ -889,18 +889,27 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
 // end of the launch.  One device-scope fetch-add (lane 0, vector memory) per
 // attempt; `gone` marks the queues found empty (wave-uniform).
 template <int W>
-__device__ __forceinline__ bool ks_take(const KeystreamArgs &A, uint64_t *ctr, uint32_t x, uint32_t l,
-                                        uint32_t &gone, uint64_t &b, uint32_t &w) {
+__device__ __forceinline__ bool ks_take(const KeystreamArgs &A, const KeystreamArgs &A2, uint64_t *ctr, uint32_t x,
+                                        uint32_t l, uint32_t &gone, uint64_t &b, uint32_t &w, bool &second) {
     for (uint32_t i = 0; i < 8; ++i) {
         const uint32_t v = (x + i) & 7;
         if (gone & (1u << v)) continue;
         const uint64_t quota = (uint64_t)W * ((A.nwg + 7 - v) / 8);
+        const uint64_t quota2 = (uint64_t)W * ((A2.nwg + 7 - v) / 8);   // A2.nwg = 0: no second set
         uint64_t q = 0;
         if (l == 0) q = __hip_atomic_fetch_add(ctr + 16 * v, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         q = readlane64(q, 0);
         if (q < quota) {
             b = 8 * (q / W) + v;
             w = (uint32_t)(q % W);
+            second = false;
+            return true;
+        }
+        if (q - quota < quota2) {
+            q -= quota;
+            b = 8 * (q / W) + v;
+            w = (uint32_t)(q % W);
+            second = true;
             return true;
         }
         gone |= 1u << v;
@@ -913,9 +922,12 @@ __device__ __forceinline__ bool ks_take(const KeystreamArgs &A, uint64_t *ctr, u
 // resident waves): gridDim.x workgroups stay resident and every wave takes
 // units from the per-XCD queues until all are empty; counter set A.par of
 // A.ctr serves this launch, and workgroup 0 zeroes the other set for the next
-// launch on the stream (launches on one stream never overlap).
+// launch on the stream (launches on one stream never overlap).  Each queue
+// holds its XCD's units of A, then its units of A2 (A2.nwg > 0: the launch's
+// last chunks with shorter lanes, so the launch drains on shorter units).
 template <int D, int W, int SP>
-__global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab) {
+__global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArgs A, const uint64_t *jtab,
+                                                      KeystreamArgs A2, const uint64_t *jtab2) {
     constexpr int RS = D * 8 + 16;
     __shared__ __attribute__((aligned(16))) uint8_t rows[W][64 * RS];
     const uint32_t t = threadIdx.x, l = t & 63;
@@ -931,7 +943,11 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
     const uint32_t x = blockIdx.x & 7;
     uint32_t gone = 0, ww = 0;
     uint64_t b = 0;
-    while (ks_take<W>(A, cur, x, l, gone, b, ww)) ks_unit<D, W, SP>(dst, A, jtab, myrows, l, ks_remap(A, b), ww);
+    bool second = false;
+    while (ks_take<W>(A, A2, cur, x, l, gone, b, ww, second)) {
+        if (second) ks_unit<D, W, SP>(dst, A2, jtab2, myrows, l, ks_remap(A2, b), ww);
+        else ks_unit<D, W, SP>(dst, A, jtab, myrows, l, ks_remap(A, b), ww);
+    }
 }
 
 // DG1 zero prefixes in the fill's store shape (paired with a keystream launch
@@ -976,16 +992,17 @@ void launch_zp_one(dim3 g, uint32_t lds, hipStream_t s, uint8_t *dst, uint64_t y
 
 template <int D, int W>
 hipError_t launch_ks_one(uint8_t *dst, const KeystreamArgs &A, const uint64_t *jtab, uint32_t lds,
-                         int store, hipStream_t s, uint64_t wgs) {
+                         int store, hipStream_t s, uint64_t wgs, const KeystreamArgs &A2, const uint64_t *jtab2) {
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const dim3 g((uint32_t)wgs), t(64 * W);
     if (store == kStoreSC1)
-        hipLaunchKernelGGL((k_keystream<D, W, kStoreSC1>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+        hipLaunchKernelGGL((k_keystream<D, W, kStoreSC1>), g, t, lds, s, dst, A, jtab, A2, jtab2);
     else if (store == kStoreNTSC1)
-        hipLaunchKernelGGL((k_keystream<D, W, kStoreNTSC1>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+        hipLaunchKernelGGL((k_keystream<D, W, kStoreNTSC1>), g, t, lds, s, dst, A, jtab, A2, jtab2);
     else if (store == kStoreNT)
-        hipLaunchKernelGGL((k_keystream<D, W, kStoreNT>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+        hipLaunchKernelGGL((k_keystream<D, W, kStoreNT>), g, t, lds, s, dst, A, jtab, A2, jtab2);
     else
-        hipLaunchKernelGGL((k_keystream<D, W, kStorePlain>), dim3((uint32_t)wgs), dim3(64 * W), lds, s, dst, A, jtab);
+        hipLaunchKernelGGL((k_keystream<D, W, kStorePlain>), g, t, lds, s, dst, A, jtab, A2, jtab2);
     return hipGetLastError();
 }
 
@@ -1230,18 +1247,31 @@ static int ks_resident_per_cu(const KsShape &sh, uint32_t lds) {
 }
 
 hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A0, const uint64_t *jtab,
-                           const KsShape &sh, hipStream_t s, KsCounters *ctrs, int cus, int persist_rounds) {
+                           const KsShape &sh, hipStream_t s, KsCounters *ctrs, int cus, int persist_rounds,
+                           const KeystreamArgs *tail, const uint64_t *tail_jtab) {
     (void)hipGetLastError();
     const uint32_t lds = occupancy_lds(sh.wgs_per_cu, ks_static_lds(sh.draws, sh.waves));
-    KeystreamArgs A = A0;
-    A.xg = sh.xcd_waves > sh.waves ? (uint32_t)(sh.xcd_waves / sh.waves) : 1u;
-    const uint64_t waves = (A.nchunks * A.lpc + 63) / 64;
-    const uint64_t wgs = (waves + sh.waves - 1) / sh.waves;
-    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    A.nwg = (uint32_t)wgs;
-    A.ctr = nullptr;
-    A.par = 0;
+    const uint32_t xg = sh.xcd_waves > sh.waves ? (uint32_t)(sh.xcd_waves / sh.waves) : 1u;
+    // static-grid workgroups of an argument set
+    auto grid_of = [&](KeystreamArgs &X) -> uint64_t {
+        X.xg = xg;
+        const uint64_t waves = (X.nchunks * X.lpc + 63) / 64;
+        const uint64_t wgs = (waves + sh.waves - 1) / sh.waves;
+        X.nwg = (uint32_t)(wgs > 0x7FFFFFFFull ? 0x7FFFFFFFull : wgs);
+        X.ctr = nullptr;
+        X.par = 0;
+        return wgs;
+    };
+    KeystreamArgs A = A0, A2{};
+    const uint64_t wgs = grid_of(A);
+    uint64_t wgs2 = 0;
+    if (tail) {
+        A2 = *tail;
+        wgs2 = grid_of(A2);
+    }
+    if (wgs > 0x7FFFFFFFull || wgs2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     uint64_t grid = wgs;
+    bool persistent = false;
 #if !S3DG_DIAG_KS_STATIC
     // at least `rounds` rounds of resident waves (default: 1-wave workgroups
     // from kKsPersistRounds): a persistent grid over per-XCD queues
@@ -1249,16 +1279,25 @@ hipError_t launch_keystream(uint8_t *dst, const KeystreamArgs &A0, const uint64_
     const uint64_t rounds = persist_rounds < 0 ? (sh.waves == 1 ? kKsPersistRounds : 0) : (uint64_t)persist_rounds;
     if (rounds > 0 && ctrs && ctrs->dev && cus > 0) {
         const uint64_t cap = ((uint64_t)ks_resident_per_cu(sh, lds) * (uint64_t)cus) & ~7ull;
-        if (cap >= 8 && wgs >= rounds * cap) {
+        if (cap >= 8 && wgs + wgs2 >= rounds * cap) {
             A.ctr = ctrs->dev;
             A.par = ctrs->par;
             grid = cap;
+            persistent = true;
         }
     }
 #endif
     hipError_t e;
-    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s, grid);
-    if (e == hipSuccess && A.ctr) ctrs->par ^= 1u;
+    if (persistent) {   // both sets in one launch, A's units first
+        S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s, grid, A2, tail_jtab);
+        if (e == hipSuccess) ctrs->par ^= 1u;
+        return e;
+    }
+    KeystreamArgs none{};   // static grid: A2 unused (nwg 0); the tail set as a launch of its own
+    S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A, jtab, lds, sh.store, s, grid, none, (const uint64_t *)nullptr);
+    if (e == hipSuccess && tail)
+        S3DG_KS_DISPATCH(e, launch_ks_one, sh, dst, A2, tail_jtab, lds, sh.store, s, wgs2, none,
+                         (const uint64_t *)nullptr);
     return e;
 }
 

@@ -208,6 +208,12 @@ class Context:
         1-wave workgroups from 6 rounds).  Results are identical."""
         call("s3dg_set_keystream_persist", self._h, int(rounds))
 
+    def set_keystream_tail(self, chunks: int = -1) -> None:
+        """One-object DG1 launches on a persistent grid: the last `chunks`
+        blocks in half-length lanes, handed out last (0 = off, negative =
+        default).  Results are identical."""
+        call("s3dg_set_keystream_tail", self._h, int(chunks))
+
     def set_dgen_zero_split(self, chunks: int = -1, waves: int = -1, occupancy: int = -1, store: int = -1,
                             overlap: int = -1) -> None:
         """DG1 launches with a zero prefix over >= `chunks` full 1 MiB blocks run

@@ -137,3 +137,22 @@ def test_zero_grid_pieces(S, one, split):
     for off in range(0, n * size, piece):
         assert torch.equal(a[off:off + piece], b[off:off + piece]), off
     del a, b
+
+
+@pytest.mark.parametrize("size,c", [(70 * MiB + 3, 2), (65 * MiB + 4095, 3)])
+def test_ragged_stream_splits_full_blocks(S, oracle, one, gpu_ctx, size, c):
+    """Objects with a short last block (the default context, >= 64 full
+    blocks per object): the full blocks split, the short last blocks in a
+    launch of their own; equal to the single launch, gaps untouched."""
+    import torch
+    stride, n, sb = 72 * MiB, 3, 0x5EED000000000001
+    a, b = _pair(torch, n * stride)
+    gpu_ctx.dgen_fill_stream(a, size, n, stride=stride, dedup=2, compress=c, seed_base=sb, first_obj=1)
+    one.dgen_fill_stream(b, size, n, stride=stride, dedup=2, compress=c, seed_base=sb, first_obj=1)
+    torch.cuda.synchronize()
+    for j in range(n):
+        assert torch.equal(a[j * stride:j * stride + size], b[j * stride:j * stride + size]), j
+        assert (a[j * stride + size:(j + 1) * stride].cpu().numpy() == 0xAB).all(), j
+    fn, fd = S.compress_ratio(c)
+    exp = oracle.dgen_fill(size, 2, fn, fd, S.object_entropy(sb, 1 + n - 1))
+    assert bytes(a[(n - 1) * stride:(n - 1) * stride + size].cpu().numpy()) == bytes(exp)

@@ -168,3 +168,25 @@ def test_persistent_fuzz_shapes(S, gpu_ctx, case):
             gpu_ctx.xoshiro_fill(b[off:], min(per, size - off), seed_base=sb + off // (2 * MiB))
     torch.cuda.synchronize()
     assert torch.equal(a, b), (mode, waves, size)
+
+
+@pytest.mark.parametrize("size,d,c", [(6 * GiB, 1, 1), (6 * GiB + 5, 2, 1), (6 * GiB, 2, 2), (5 * GiB, 1, 3)])
+def test_tail_half_lanes_equal(S, gpu_ctx, size, d, c):
+    """One-object DG1 launches on the persistent grid hand out their last
+    blocks as half-length lanes (s3dg_set_keystream_tail): the default, a
+    long tail (1000 blocks) and none (0: the round-4 launch, pinned to the
+    oracle by the tests above) write the same bytes, and nothing past the
+    object."""
+    import torch
+    outs = []
+    for tail in (-1, 1000, 0):
+        ctx = S.Context(0, base_seed=S.DEFAULT_BASE_SEED)
+        ctx.set_keystream_tail(tail)
+        a = torch.full((size + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+        ctx.dgen_fill(a, size, dedup=d, compress=c, seed=0xBEEF + c)
+        torch.cuda.synchronize()
+        outs.append(a)
+        ctx.close()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert (outs[0][size:].cpu().numpy() == 0xAB).all()
+    del outs

@@ -8,7 +8,7 @@ s3dg_dgen_fill_stream launch) at the given compress (default 1 for 14/16, 2
 for 15/17), timed with HIP events; mean GB/s over the samples.
 
     python tools/dg1_split_lab.py          # GPU box
-LAB_SETTINGS: "name=chunks/waves/occ/store/overlap[/xcd_group[/lane_draws]];..." (default below), LAB_POINTS:
+LAB_SETTINGS: "name=chunks/waves/occ/store/overlap[/xcd_group[/lane_draws[/tail]]];..." (default below), LAB_POINTS:
 "cfg15@2;cfg17@2;cfg15@3" (@compress), LAB_REPS (default 6).
 Tooling only: nothing in the product imports this."""
 import json, os, statistics, sys
@@ -34,6 +34,8 @@ def main():
             c.set_keystream_xcd_group(1, f[5])
         if len(f) > 6 and f[6]:          # DG1 keystream draws per lane (tails: lanes of a 64-lane wave)
             c.set_keystream_shape(1, 0, 0, 0, f[6], -1)
+        if len(f) > 7:                   # one-object launches' half-lane tail blocks (s3dg_set_keystream_tail)
+            c.set_keystream_tail(f[7])
         sets[name] = c
     pts = os.environ.get("LAB_POINTS", "cfg15@2;cfg17@2;cfg15@3;cfg17@3").split(";")
     reps = int(os.environ.get("LAB_REPS", "6"))
