@@ -11,7 +11,7 @@ the fastest setting's p10, and the amdsmi power, GFX clock and PPT residency
 during its blocks.
 
     python tools/dip_lab.py        # GPU box; LAB_SETTINGS "name=pace/occ;...",
-                                   # LAB_POINT cfg2 (default) | cfg4 | cfg8
+                                   # LAB_POINT cfg2 (default) | cfg3 | cfg4 | cfg8
 Tooling only: nothing in the product imports this."""
 import ctypes, json, os, statistics, sys, threading, time
 
@@ -63,6 +63,9 @@ def main():
                                                 u32(1), u64(0x5EED000000000001), u64(0), sh)
         elif point == "cfg4":
             r = lib.s3dg_fill_controlled_batch(h, p, arr, u64(n), sh)
+        elif point == "cfg3":  # config 3: 10 000 x 8 MiB, d4 c2
+            r = lib.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(4), u32(1), u32(2),
+                                                u64(0x5EED000000000001), u64(0), sh)
         else:
             r = lib.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(1), u32(0), u32(1),
                                                 u64(0x5EED000000000001), u64(0), sh)
