@@ -66,19 +66,27 @@ Poly berlekamp_massey(const std::vector<uint8_t> &s) {
     return P;
 }
 
+// r ^= p * x^sh (word-wise shift-xor; r long enough)
+void xor_shifted(Poly &r, const Poly &p, int sh) {
+    const int wo = sh >> 6, bo = sh & 63;
+    for (size_t j = 0; j < p.size(); ++j) {
+        if (!p[j]) continue;
+        r[wo + j] ^= p[j] << bo;
+        if (bo) r[wo + j + 1] ^= p[j] >> (64 - bo);
+    }
+}
+
+// a * b mod P over GF(2): one shift-xor of b per set bit of a, then one of P
+// per set bit at or above x^dP (round 5: word-wise, ~40x faster than bit by
+// bit: 0.08 ms per jump polynomial instead of 3 ms)
 Poly mulmod(const Poly &a, const Poly &b, const Poly &P, int dP) {
-    Poly r((2 * dP + 127) / 64 + 1, 0);
-    const int db = degree(b);
-    for (int i = 0; i <= degree(a); ++i) {
-        if (!bit(a, i)) continue;
-        for (int k = 0; k <= db; ++k)
-            if (bit(b, k)) setbit(r, i + k);
-    }
-    for (int i = degree(r); i >= dP; --i) {
-        if (!bit(r, i)) continue;
-        for (int k = 0; k <= dP; ++k)
-            if (bit(P, k)) setbit(r, i - dP + k);
-    }
+    const int da = degree(a), db = degree(b);
+    Poly r((size_t)((da > 0 ? da : 0) + (db > 0 ? db : 0) + 64) / 64 + 2 + P.size(), 0);
+    if (da >= 0 && db >= 0)
+        for (int i = 0; i <= da; ++i)
+            if (bit(a, i)) xor_shifted(r, b, i);
+    for (int i = degree(r); i >= dP; --i)
+        if (bit(r, i)) xor_shifted(r, P, i - dP);
     r.resize((dP + 63) / 64, 0);
     return r;
 }
@@ -117,6 +125,14 @@ bool jump_poly(uint64_t n, uint64_t out[4]) {
         n >>= 1;
     }
     for (int k = 0; k < 4; ++k) out[k] = k < (int)result.size() ? result[k] : 0;
+    return true;
+}
+
+bool jump_mul(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]) {
+    const Engine &E = engine();
+    if (E.dP != 256) return false;
+    const Poly r = mulmod(Poly(a, a + 4), Poly(b, b + 4), E.P, E.dP);
+    for (int k = 0; k < 4; ++k) out[k] = k < (int)r.size() ? r[k] : 0;
     return true;
 }
 

@@ -9,4 +9,6 @@ int xoshiro_poly_degree();
 bool jump_poly(uint64_t n, uint64_t out[4]);
 // s <- T^n s for the n that produced J (host reference of the device jump).
 void apply_jump(uint64_t s[4], const uint64_t J[4]);
+// out = a * b mod P: the jump by n + m from the jumps by n and by m
+bool jump_mul(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
 }  // namespace s3dg

@@ -874,9 +874,14 @@ __device__ __forceinline__ void ks_unit(uint8_t *dst, const KeystreamArgs &A, co
     }
 #if S3DG_KS_TRACE
     if (l == 0 && g_ks_trace) {
-        const uint64_t wi = bid * W + w;
-        g_ks_trace[2 * wi] = t_start;
-        g_ks_trace[2 * wi + 1] = wall_clock64();
+        // bits 48-63: HW_ID's wave/SIMD/pipe/CU/SH/SE fields (start stamp),
+        // XCC_ID (end stamp); the 100 MHz clock below (tools/ks_xcd_lab.py)
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const uint64_t wi = bid * W + w, m48 = (1ull << 48) - 1;
+        g_ks_trace[2 * wi] = (t_start & m48) | ((uint64_t)(hw & 0xFFFFu) << 48);
+        g_ks_trace[2 * wi + 1] = (wall_clock64() & m48) | ((uint64_t)(xcc & 0xFu) << 48);
     }
 #endif
 }

@@ -8,8 +8,9 @@ s3dg_dgen_fill_stream launch) at the given compress (default 1 for 14/16, 2
 for 15/17), timed with HIP events; mean GB/s over the samples.
 
     python tools/dg1_split_lab.py          # GPU box
-LAB_SETTINGS: "name=chunks/waves/occ/store/overlap[/xcd_group[/lane_draws[/tail]]];..." (default below), LAB_POINTS:
-"cfg15@2;cfg17@2;cfg15@3" (@compress), LAB_REPS (default 6).
+LAB_SETTINGS: "name=chunks/waves/occ/store/overlap[/xcd_group[/lane_draws[/tail]]];..." (default
+below), LAB_POINTS: "cfg15@2;cfg17@2;cfg15@3" (@compress; cfg6:
+config 6's K2 launch, 84 GB as 2 MiB Xoshiro256++ chunks), LAB_REPS (default 6).
 Tooling only: nothing in the product imports this."""
 import json, os, statistics, sys
 
@@ -43,6 +44,9 @@ def main():
     G8 = 8 * GiB
 
     def run(c, kind, comp):
+        if kind == "cfg6":                                  # config 6: 10 000 x 8 MiB as 2 MiB keystream chunks
+            c.xoshiro_fill(buf, 10000 * 8 * (1 << 20), 2 << 20, 0x5EED)
+            return
         d = 2 if kind in ("cfg15", "cfg17") else 1          # configs 14 / 16: dedup 1
         if kind in ("cfg14", "cfg15"):                      # one launch per 8 GiB object
             for t in range(10):
@@ -76,8 +80,9 @@ def main():
         for n in names:
             ms = res[(n, p)]
             mean = sum(ms) / len(ms)
-            print(json.dumps({"setting": n, "point": p, "GBps_mean": round(80 * GiB / (mean * 1e-3) / 1e9, 1),
-                              "frac": round(80 * GiB / (mean * 1e-3) / 8e12, 4),
+            nb = 10000 * 8 * (1 << 20) if p.startswith("cfg6") else 80 * GiB
+            print(json.dumps({"setting": n, "point": p, "GBps_mean": round(nb / (mean * 1e-3) / 1e9, 1),
+                              "frac": round(nb / (mean * 1e-3) / 8e12, 4),
                               "ms_mean": round(mean, 3), "ms_min": round(min(ms), 3),
                               "ms_median": round(statistics.median(ms), 3), "n": len(ms)}), flush=True)
 

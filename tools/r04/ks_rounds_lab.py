@@ -26,7 +26,8 @@ def analyse(trace, name, event_ms, nbytes):
     # XCD of trace slot wi (1-wave workgroups, XCD groups of 16): the remap puts
     # the 16 units of XCD x at bid = 128 * (k >> 4) + 16 * x + (k & 15)
     wi = np.nonzero(t[:, 1] > 0)[0]
-    xcd = (wi >> 4) & 7
+    xg = int(os.environ.get("LAB_XG", "16"))
+    xcd = (wi // xg) & 7
     t = t[t[:, 1] > 0]
     t0 = t[:, 0].min()
     per_xcd = {}
@@ -51,7 +52,16 @@ def analyse(trace, name, event_ms, nbytes):
     # time the chip is not full at the end: from the last moment >= 95 % busy to the last wave's end
     busy = [i for i, a in enumerate(active) if a >= 0.95 * full]
     tail_us = span - float(bins[busy[-1] + 1]) if busy else None
-    return {"case": name, "event_ms": round(event_ms, 3), "GBps": round(nbytes / event_ms / 1e6, 1),
+    # units in flight over the last 200 us, 10-us bins (end of launch)
+    tb = np.arange(span - 200.0, span, 10.0)
+    end_profile = [int(((s <= b) & (e > b)).sum()) for b in tb]
+    # the first unit each resident slot ran vs the rest (ramp cost per unit)
+    first = dur[order[:full]]
+    rest = dur[order[full:]]
+    return {"case": name, "end_profile_10us": end_profile,
+            "first_round_us_median": round(float(np.median(first)), 1),
+            "later_units_us_median": round(float(np.median(rest)), 1) if len(rest) else None,
+            "unit_us_p5_p95": [round(float(np.quantile(dur, 0.05)), 1), round(float(np.quantile(dur, 0.95)), 1)], "event_ms": round(event_ms, 3), "GBps": round(nbytes / event_ms / 1e6, 1),
             "waves": int(len(s)), "resident": full, "span_us": round(span, 1),
             "event_minus_span_us": round(event_ms * 1e3 - span, 1), "occupancy_area": round(area, 4),
             "tail_not_full_us": round(tail_us, 1) if tail_us is not None else None,
@@ -65,11 +75,19 @@ def main():
                     mode=os.RTLD_LOCAL)
     h = ctypes.c_void_p()
     assert L.s3dg_ctx_create(0, ctypes.byref(h)) == 0
+    if os.environ.get("LAB_TAIL"):      # round 5: tail chunks of half-length units (0: none, so slots do not collide)
+        assert L.s3dg_set_keystream_tail(h, ctypes.c_int(int(os.environ["LAB_TAIL"]))) == 0
+    if os.environ.get("LAB_XG"):        # units per XCD group of the remap (1: plain round-robin dealing)
+        assert L.s3dg_set_keystream_xcd_group(h, 1, ctypes.c_uint32(int(os.environ["LAB_XG"]))) == 0
     u64, u32 = ctypes.c_uint64, ctypes.c_uint32
     st = torch.cuda.current_stream()
     sh = ctypes.c_void_p(st.cuda_stream)
     n_obj = 10
-    buf = torch.empty(n_obj * 8 * GiB, dtype=torch.uint8, device="cuda")
+    # LAB_SHIFT_MIB: every launch's dst moved up by that many MiB (round 5: do
+    # the slow unit groups follow the addresses they write or the XCDs?)
+    shift = int(os.environ.get("LAB_SHIFT_MIB", "0")) * MiB
+    buf0 = torch.empty(n_obj * 8 * GiB + shift, dtype=torch.uint8, device="cuda")
+    buf = buf0[shift:]
     trace = torch.zeros(2 * (n_obj * 8 * GiB // MiB) * 2, dtype=torch.int64, device="cuda")
     assert L.s3dg_diag_ks_trace(ctypes.c_void_p(trace.data_ptr())) == 0
     SEED = 0x5EED000000000001
