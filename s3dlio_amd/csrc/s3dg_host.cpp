@@ -41,6 +41,7 @@
 #include <time.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -454,9 +455,15 @@ bool host_register_on() {
     return on;
 }
 
+struct UserReg {
+    uint64_t bytes;    // page-rounded length
+    uint8_t *dev;      // device pointer of the first page
+    int users;         // host calls in flight on it (they hold it until they return)
+};
 struct UserRegs {
     std::mutex mu;
-    std::map<uintptr_t, std::pair<uint64_t, uint8_t *>> regs;   // page start -> (bytes, device pointer of start)
+    std::condition_variable cv;                      // a registration's users dropped to 0
+    std::map<uintptr_t, UserReg> regs;               // page start -> registration
     std::map<std::pair<uintptr_t, uint64_t>, int> seen;
     uint64_t bytes = 0;
 };
@@ -465,34 +472,68 @@ UserRegs &userregs() {
     return *r;
 }
 
+// Unregisters every registration matching `hit` once no call uses it (R.mu
+// held through `g`, released while waiting).  Returns how many it dropped.
+template <class Hit>
+int drop_regs(UserRegs &R, std::unique_lock<std::mutex> &g, Hit hit) {
+    int dropped = 0;
+    for (;;) {
+        bool busy = false;
+        for (auto q = R.regs.begin(); q != R.regs.end();) {
+            if (!hit(q->first, q->second.bytes)) {
+                ++q;
+            } else if (q->second.users > 0) {
+                busy = true;
+                ++q;
+            } else {
+                (void)hipHostUnregister((void *)q->first);
+                (void)hipGetLastError();
+                R.bytes -= q->second.bytes;
+                q = R.regs.erase(q);
+                ++dropped;
+            }
+        }
+        if (!busy) return dropped;
+        R.cv.wait(g);   // another thread's call is writing into one of them
+    }
+}
+
+// A host call's hold on a registered range (UserHold::key != 0), released
+// when the call returns.
+struct UserHold {
+    uintptr_t key = 0;
+    ~UserHold() {
+        if (!key) return;
+        UserRegs &R = userregs();
+        std::lock_guard<std::mutex> g(R.mu);
+        auto it = R.regs.find(key);
+        if (it != R.regs.end() && --it->second.users == 0) R.cv.notify_all();
+    }
+};
+
 // The device pointer of [p, p+n) when it lies in a registered range; on the
 // second call with this (p, n), registers its pages first (may_register: the
-// call can take the direct path).  A range that overlaps registered ones
-// without lying inside one unregisters them first: HIP treats a copy into a
-// partly registered range as pinned and fails.  Host calls are synchronous,
-// so nothing is in flight on a range when it is dropped.  nullptr: use the
-// regular paths.
-uint8_t *user_registered(const uint8_t *p, uint64_t n, bool may_register) {
+// call can take the direct path).  A call inside a registered range holds it
+// (hold) until it returns, direct or not, so no other thread unregisters pages
+// it is writing.  A range that overlaps registered ones without lying inside
+// one unregisters them first, once their holders have returned: HIP treats a
+// copy into a partly registered range as pinned and fails (two threads'
+// buffers can share a page).  nullptr: use the regular paths.
+uint8_t *user_registered(const uint8_t *p, uint64_t n, bool may_register, UserHold &hold) {
     UserRegs &R = userregs();
     const uintptr_t a = (uintptr_t)p;
-    std::lock_guard<std::mutex> g(R.mu);
+    std::unique_lock<std::mutex> g(R.mu);
     auto it = R.regs.upper_bound(a);
     if (it != R.regs.begin()) {
         --it;
-        if (a >= it->first && a + n <= it->first + it->second.first)
-            return may_register ? it->second.second + (a - it->first) : nullptr;
-    }
-    const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
-    for (auto q = R.regs.begin(); q != R.regs.end();) {   // drop the registrations this range overlaps
-        if (q->first < hi && q->first + q->second.first > lo) {
-            (void)hipHostUnregister((void *)q->first);
-            (void)hipGetLastError();
-            R.bytes -= q->second.first;
-            q = R.regs.erase(q);
-        } else {
-            ++q;
+        if (a >= it->first && a + n <= it->first + it->second.bytes) {
+            ++it->second.users;
+            hold.key = it->first;
+            return may_register ? it->second.dev + (a - it->first) : nullptr;
         }
     }
+    const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
+    drop_regs(R, g, [&](uintptr_t s0, uint64_t len) { return s0 < hi && s0 + len > lo; });
     if (!may_register) return nullptr;
     if (R.seen.size() >= kRegSeenMax) R.seen.clear();
     if (++R.seen[{a, n}] < 2) return nullptr;
@@ -507,30 +548,20 @@ uint8_t *user_registered(const uint8_t *p, uint64_t n, bool may_register) {
         (void)hipHostUnregister((void *)lo);
         return nullptr;
     }
-    R.regs[lo] = {hi - lo, (uint8_t *)d};
+    R.regs[lo] = UserReg{hi - lo, (uint8_t *)d, 1};
     R.bytes += hi - lo;
     R.seen.erase({a, n});
+    hold.key = lo;
     return (uint8_t *)d + (a - lo);
 }
 }  // namespace
 
 extern "C" int s3dg_host_unregister(void *buf) {
     UserRegs &R = userregs();
-    std::lock_guard<std::mutex> g(R.mu);
-    int released = 0;
-    for (auto it = R.regs.begin(); it != R.regs.end();) {
-        const uintptr_t a = (uintptr_t)buf;
-        if (!buf || (a >= it->first && a < it->first + it->second.first)) {
-            // kernels that wrote into it were waited for by the call that launched them
-            (void)hipHostUnregister((void *)it->first);
-            (void)hipGetLastError();
-            R.bytes -= it->second.first;
-            it = R.regs.erase(it);
-            ++released;
-        } else {
-            ++it;
-        }
-    }
+    std::unique_lock<std::mutex> g(R.mu);
+    const uintptr_t a = (uintptr_t)buf;
+    // waits for calls still writing into a matching range (other threads')
+    const int released = drop_regs(R, g, [&](uintptr_t s0, uint64_t len) { return !buf || (a >= s0 && a < s0 + len); });
     R.seen.clear();
     return released;
 }
@@ -657,9 +688,10 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     H_TRY(ds.err, "hipSetDevice");
     bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
     uint8_t *kdst = buf;
+    UserHold hold;   // released on return: the call's copies and kernels are done by then
     if (!direct && host_register_on()) {
         const bool geo = !d2h_staged() && direct_geometry(J, buf, pos, n);
-        if (uint8_t *d = user_registered(buf, n, geo)) {   // a repeated pageable buffer, now page-locked
+        if (uint8_t *d = user_registered(buf, n, geo, hold)) {   // a repeated pageable buffer, now page-locked
             direct = true;
             kdst = d;
         }

@@ -297,3 +297,44 @@ def test_registered_pageable_buffer_child(oracle, golden_base):
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "registered ok" in out.stdout
+
+
+def test_registered_buffers_sharing_a_page_child(oracle, golden_base):
+    """S3DLIO_HOST_REGISTER=1 (child process), four threads whose buffers share
+    their boundary pages (one array cut at offsets that are not page
+    multiples), each calling fill_controlled_data on its own buffer eight
+    times: registering one thread's pages would drop a neighbour's overlapping
+    registration, so a call holds its registered range until it returns and an
+    overlapping call waits for it.  Every call's bytes equal the oracle's and
+    nothing outside the buffers changes."""
+    code = (
+        "import ctypes, threading, numpy as np, sys; sys.path.insert(0, %r)\n"
+        "from s3dlio_amd._lib import lib as L\n"
+        "from oracle import oracle_c as OC\n"
+        "gb = np.frombuffer(open(%r, 'rb').read(), np.uint8)\n"
+        "base = (ctypes.c_uint8 * 4096).from_buffer_copy(gb.tobytes())\n"
+        "MiB = 1 << 20; T = 4; size = MiB + 2048; g = 8192\n"
+        "raw = np.full(T * size + 2 * g + 4096, 0xA5, np.uint8)\n"
+        "o0 = (-raw.ctypes.data) %% 4096 + g + 1024\n"
+        "exp = {}\n"
+        "for t in range(T):\n"
+        "    for k in range(8): exp[(t, k)] = bytes(OC.fill_controlled(size, 1, 0, 1, 1000 * t + k, gb))\n"
+        "errs = []\n"
+        "def worker(t):\n"
+        "    try:\n"
+        "        o = o0 + t * size\n"
+        "        for k in range(8):\n"
+        "            assert L.s3dlio_fill_controlled_data_seeded(raw.ctypes.data + o, size, 1, 1, 1000 * t + k, base) == 0\n"
+        "            assert bytes(raw[o:o + size]) == exp[(t, k)], (t, k)\n"
+        "    except Exception as e:\n"
+        "        errs.append(repr(e))\n"
+        "ts = [threading.Thread(target=worker, args=(t,)) for t in range(T)]\n"
+        "[x.start() for x in ts]; [x.join() for x in ts]\n"
+        "assert not errs, errs\n"
+        "assert (raw[:o0] == 0xA5).all() and (raw[o0 + T * size:] == 0xA5).all()\n"
+        "L.s3dg_host_unregister(None)\n"
+        "print('shared pages ok')\n" % (ROOT, os.path.join(ROOT, "tests", "golden", "base_block_ba5eb10c.bin")))
+    env = dict(os.environ, S3DLIO_HOST_REGISTER="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "shared pages ok" in out.stdout
