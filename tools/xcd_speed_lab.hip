@@ -1,0 +1,82 @@
+// xcd_speed_lab.hip — diagnostic kernels (tools/xcd_speed_lab.py; not product
+// code): is the keystream's slower half of XCDs
+// slower at arithmetic or at stores?  1-wave workgroups, four per CU (the
+// keystream's residency), each wave timing its own work with the 100 MHz
+// wall clock and recording the XCC that ran it:
+//   k_valu         Xoshiro256 state steps in registers (no memory traffic)
+//   k_store_seq    whole 1 KiB per store instruction, each wave a contiguous run
+//   k_store_lanes  the keystream's pattern: 64 lane regions per wave, 512-B
+//                  pieces, two rows per store instruction
+// Stores are global_store_dwordx4 ... sc1, as the product's.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void st_sc1(uint8_t *p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void stamp(uint64_t *out, uint64_t t0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (threadIdx.x == 0) {
+        out[3 * blockIdx.x] = t0;
+        out[3 * blockIdx.x + 1] = wall_clock64();
+        out[3 * blockIdx.x + 2] = xcc;
+    }
+}
+
+__device__ __forceinline__ uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+__global__ __launch_bounds__(64) void k_valu(uint64_t *out, uint64_t *sink, uint32_t iters) {
+    const uint64_t t0 = wall_clock64();
+    uint64_t s0 = threadIdx.x + 1, s1 = blockIdx.x * 77 + 3, s2 = 0x9E3779B97F4A7C15ull, s3 = 12345;
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        acc += rotl(s0 + s3, 23) + s0;
+        const uint64_t t = s1 << 17;
+        s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45);
+    }
+    if (acc == 0x12345) sink[blockIdx.x] = acc;   // keeps the loop
+    stamp(out, t0);
+}
+
+__global__ __launch_bounds__(64) void k_store_seq(uint8_t *dst, uint64_t *out, uint64_t bpw, uint32_t units) {
+    const uint64_t t0 = wall_clock64();
+    const u32x4 v = {threadIdx.x * 0x01010101u, blockIdx.x, 0x5A5A5A5Au, ~threadIdx.x};
+    for (uint32_t u = 0; u < units; ++u) {
+        uint8_t *base = dst + ((uint64_t)u * gridDim.x + blockIdx.x) * bpw;
+        for (uint64_t o = threadIdx.x * 16; o < bpw; o += 1024) st_sc1(base + o, v);
+    }
+    stamp(out, t0);
+}
+
+__global__ __launch_bounds__(64) void k_store_lanes(uint8_t *dst, uint64_t *out, uint32_t span, uint32_t units) {
+    const uint64_t t0 = wall_clock64();
+    const uint32_t l = threadIdx.x, piece = l % 32;
+    const u32x4 v = {l * 0x01010101u, blockIdx.x, 0xA5A5A5A5u, ~l};
+    for (uint32_t u = 0; u < units; ++u) {
+        uint8_t *base = dst + ((uint64_t)u * gridDim.x + blockIdx.x) * 64ull * span;
+        for (uint32_t it = 0; it < span / 512; ++it)
+            for (int i = 0; i < 32; ++i) st_sc1(base + (uint64_t)(2 * i + l / 32) * span + it * 512 + piece * 16, v);
+    }
+    stamp(out, t0);
+}
+
+extern "C" {
+int lab_valu(void *out, void *sink, uint32_t grid, uint32_t iters, void *s) {
+    hipLaunchKernelGGL(k_valu, dim3(grid), dim3(64), 0, (hipStream_t)s, (uint64_t *)out, (uint64_t *)sink, iters);
+    return (int)hipGetLastError();
+}
+int lab_store_seq(void *dst, void *out, uint32_t grid, uint64_t bpw, uint32_t units, uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_seq, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out, bpw,
+                       units);
+    return (int)hipGetLastError();
+}
+int lab_store_lanes(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_lanes, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out,
+                       span, units);
+    return (int)hipGetLastError();
+}
+}

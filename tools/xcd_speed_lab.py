@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Are the keystream's slow XCDs (queues 1/3/5/7) slow at
+arithmetic or at stores?  tools/xcd_speed_lab.hip: 1024 one-wave workgroups
+(four per CU, as the keystream; dynamic LDS caps residency at four) run
+(a) register-only Xoshiro steps, (b) contiguous 1 KiB stores, (c) the
+keystream's 64-lane-region store pattern, each wave timing itself and
+recording its XCC.  Per kernel: mean wave duration per XCC, odd/even ratio.
+
+    python tools/xcd_speed_lab.py --build    # here
+    python tools/xcd_speed_lab.py            # GPU box
+Tooling only: nothing in the product imports this."""
+import ctypes, json, os, statistics, subprocess, sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tools", "_build")
+LIB = os.path.join(OUT, "libxcdspeed.so")
+MiB = 1 << 20
+
+
+def build():
+    os.makedirs(OUT, exist_ok=True)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                           "-o", LIB, os.path.join(ROOT, "tools", "xcd_speed_lab.hip")])
+
+
+def main():
+    if "--build" in sys.argv:
+        build()
+        return
+    import torch
+    L = ctypes.CDLL(LIB)
+    u32, u64, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+    L.lab_valu.argtypes = [vp, vp, u32, u32, vp]
+    L.lab_store_seq.argtypes = [vp, vp, u32, u64, u32, u32, vp]
+    L.lab_store_lanes.argtypes = [vp, vp, u32, u32, u32, u32, vp]
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    grid = 4 * cus
+    lds = 40 * 1024            # 4 workgroups per CU (160 KiB)
+    units = 8
+    span = 16384               # 16 KiB lane regions (the keystream's 2048 draws)
+    need = units * grid * 64 * span
+    buf = torch.empty(need, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(3 * grid, dtype=torch.int64, device="cuda")
+    sink = torch.zeros(grid, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream()
+    sh = vp(st.cuda_stream)
+    kinds = {
+        "valu": lambda: L.lab_valu(vp(out.data_ptr()), vp(sink.data_ptr()), grid, 200000, sh),
+        "store_seq": lambda: L.lab_store_seq(vp(buf.data_ptr()), vp(out.data_ptr()), grid, 64 * span, units, lds, sh),
+        "store_lanes": lambda: L.lab_store_lanes(vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh),
+    }
+    res = {}
+    for rep in range(int(os.environ.get("LAB_REPS", "5"))):
+        for name, f in kinds.items():
+            assert f() == 0
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            assert f() == 0
+            e1.record(st)
+            torch.cuda.synchronize()
+            t = out.view(-1, 3).cpu().tolist()
+            per = {}
+            for s, e, x in t:
+                per.setdefault(x, []).append((e - s) * 0.01)
+            res.setdefault(name, []).append((e0.elapsed_time(e1), {x: statistics.mean(v) for x, v in per.items()},
+                                             {x: len(v) for x, v in per.items()}))
+        print(f"rep {rep} done", flush=True)
+    for name, v in res.items():
+        xs = sorted(v[0][1])
+        mean_x = {x: round(statistics.mean(r[1][x] for r in v), 2) for x in xs}
+        odd = statistics.mean(mean_x[x] for x in xs if x % 2)
+        even = statistics.mean(mean_x[x] for x in xs if x % 2 == 0)
+        line = {"kernel": name, "event_ms": [round(r[0], 3) for r in v], "wave_us_mean_by_xcc": mean_x,
+                "waves_by_xcc": v[0][2], "odd_over_even": round(odd / even, 4)}
+        if name != "valu":
+            line["GBps"] = round(need / (statistics.median(r[0] for r in v) * 1e-3) / 1e9, 1)
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
