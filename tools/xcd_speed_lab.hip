@@ -7,6 +7,7 @@
 //   k_store_seq    whole 1 KiB per store instruction, each wave a contiguous run
 //   k_store_lanes  the keystream's pattern: 64 lane regions per wave, 512-B
 //                  pieces, two rows per store instruction
+//   k_store_xcd    the fill's pattern: each wave's XCD on every 8th 4 KiB granule
 // Stores are global_store_dwordx4 ... sc1, as the product's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -64,7 +65,25 @@ __global__ __launch_bounds__(64) void k_store_lanes(uint8_t *dst, uint64_t *out,
     stamp(out, t0);
 }
 
+// every wave's XCD on every 8th 4 KiB granule (the fill's pattern): wave b
+// (dealt to XCD b mod 8) writes 1 MiB per unit as 256 granules = b (mod 8)
+__global__ __launch_bounds__(64) void k_store_xcd(uint8_t *dst, uint64_t *out, uint32_t units) {
+    const uint64_t t0 = wall_clock64();
+    const u32x4 v = {threadIdx.x * 0x01010101u, blockIdx.x, 0x3C3C3C3Cu, ~threadIdx.x};
+    const uint64_t r = blockIdx.x & 7, q = blockIdx.x >> 3, per_round = gridDim.x >> 3;
+    for (uint32_t u = 0; u < units; ++u)
+        for (uint32_t k = 0; k < 256; ++k) {
+            uint8_t *g = dst + ((((uint64_t)u * per_round + q) * 256 + k) * 8 + r) * 4096;
+            for (int i = 0; i < 4; ++i) st_sc1(g + threadIdx.x * 16 + 1024 * i, v);
+        }
+    stamp(out, t0);
+}
+
 extern "C" {
+int lab_store_xcd(void *dst, void *out, uint32_t grid, uint32_t units, uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_xcd, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out, units);
+    return (int)hipGetLastError();
+}
 int lab_valu(void *out, void *sink, uint32_t grid, uint32_t iters, void *s) {
     hipLaunchKernelGGL(k_valu, dim3(grid), dim3(64), 0, (hipStream_t)s, (uint64_t *)out, (uint64_t *)sink, iters);
     return (int)hipGetLastError();

@@ -3,7 +3,8 @@
 arithmetic or at stores?  tools/xcd_speed_lab.hip: 1024 one-wave workgroups
 (four per CU, as the keystream; dynamic LDS caps residency at four) run
 (a) register-only Xoshiro steps, (b) contiguous 1 KiB stores, (c) the
-keystream's 64-lane-region store pattern, each wave timing itself and
+keystream's 64-lane-region store pattern, (d) the fill's pattern (each XCD on
+every 8th 4 KiB granule), each wave timing itself and
 recording its XCC.  Per kernel: mean wave duration per XCC, odd/even ratio.
 
     python tools/xcd_speed_lab.py --build    # here
@@ -33,22 +34,27 @@ def main():
     L.lab_valu.argtypes = [vp, vp, u32, u32, vp]
     L.lab_store_seq.argtypes = [vp, vp, u32, u64, u32, u32, vp]
     L.lab_store_lanes.argtypes = [vp, vp, u32, u32, u32, u32, vp]
+    L.lab_store_xcd.argtypes = [vp, vp, u32, u32, u32, vp]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    grid = 4 * cus
-    lds = 40 * 1024            # 4 workgroups per CU (160 KiB)
-    units = 8
     span = 16384               # 16 KiB lane regions (the keystream's 2048 draws)
-    need = units * grid * 64 * span
+    need = 8 * 4 * cus * 64 * span
     buf = torch.empty(need, dtype=torch.uint8, device="cuda")
-    out = torch.zeros(3 * grid, dtype=torch.int64, device="cuda")
-    sink = torch.zeros(grid, dtype=torch.int64, device="cuda")
+    out = torch.zeros(3 * 32 * cus, dtype=torch.int64, device="cuda")
+    sink = torch.zeros(32 * cus, dtype=torch.int64, device="cuda")
     st = torch.cuda.current_stream()
     sh = vp(st.cuda_stream)
-    kinds = {
-        "valu": lambda: L.lab_valu(vp(out.data_ptr()), vp(sink.data_ptr()), grid, 200000, sh),
-        "store_seq": lambda: L.lab_store_seq(vp(buf.data_ptr()), vp(out.data_ptr()), grid, 64 * span, units, lds, sh),
-        "store_lanes": lambda: L.lab_store_lanes(vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh),
-    }
+    kinds = {"valu": lambda: L.lab_valu(vp(out.data_ptr()), vp(sink.data_ptr()), 4 * cus, 200000, sh)}
+    # LAB_WPC: waves (1-wave workgroups) per CU for the store kernels, capped by
+    # dynamic LDS; the same bytes at every residency (units = 32 / wpc)
+    for wpc in [int(x) for x in os.environ.get("LAB_WPC", "4").split(",")]:
+        grid, units, lds = wpc * cus, 32 // wpc, (160 // wpc) * 1024
+        sfx = "" if wpc == 4 else f"_{wpc}pcu"
+        kinds["store_seq" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_seq(
+            vp(buf.data_ptr()), vp(out.data_ptr()), grid, 64 * span, units, lds, sh))
+        kinds["store_lanes" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_lanes(
+            vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh))
+        kinds["store_xcd" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_xcd(
+            vp(buf.data_ptr()), vp(out.data_ptr()), grid, units, lds, sh))
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "5"))):
         for name, f in kinds.items():
@@ -59,7 +65,8 @@ def main():
             assert f() == 0
             e1.record(st)
             torch.cuda.synchronize()
-            t = out.view(-1, 3).cpu().tolist()
+            t = [r for r in out.view(-1, 3).cpu().tolist() if r[1] > 0]
+            out.zero_()
             per = {}
             for s, e, x in t:
                 per.setdefault(x, []).append((e - s) * 0.01)
