@@ -55,6 +55,16 @@ def main():
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh))
         kinds["store_xcd" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_xcd(
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, units, lds, sh))
+    # LAB_SHORT: the lane pattern as one unit per workgroup over a grid of many
+    # (lane region bytes per entry), like the keystream's static grid / the
+    # fill's short workgroups, four resident per CU
+    short = [int(x) for x in os.environ.get("LAB_SHORT", "").split(",") if x]
+    if short:
+        out = torch.zeros(3 * (need // (64 * min(short))), dtype=torch.int64, device="cuda")
+    for sp in short:
+        g = need // (64 * sp)
+        kinds[f"store_lanes_short_{sp // 1024}k"] = (lambda g=g, sp=sp: L.lab_store_lanes(
+            vp(buf.data_ptr()), vp(out.data_ptr()), g, sp, 1, 40 * 1024, sh))
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "5"))):
         for name, f in kinds.items():
@@ -67,11 +77,13 @@ def main():
             torch.cuda.synchronize()
             t = [r for r in out.view(-1, 3).cpu().tolist() if r[1] > 0]
             out.zero_()
-            per = {}
+            per, last = {}, {}
+            t_first = min(r[0] for r in t)
             for s, e, x in t:
                 per.setdefault(x, []).append((e - s) * 0.01)
+                last[x] = max(last.get(x, 0), (e - t_first) * 0.01)
             res.setdefault(name, []).append((e0.elapsed_time(e1), {x: statistics.mean(v) for x, v in per.items()},
-                                             {x: len(v) for x, v in per.items()}))
+                                             {x: len(v) for x, v in per.items()}, last))
         print(f"rep {rep} done", flush=True)
     for name, v in res.items():
         xs = sorted(v[0][1])
@@ -79,6 +91,7 @@ def main():
         odd = statistics.mean(mean_x[x] for x in xs if x % 2)
         even = statistics.mean(mean_x[x] for x in xs if x % 2 == 0)
         line = {"kernel": name, "event_ms": [round(r[0], 3) for r in v], "wave_us_mean_by_xcc": mean_x,
+                "xcc_last_end_us": {x: round(statistics.mean(r[3][x] for r in v), 1) for x in xs},
                 "waves_by_xcc": v[0][2], "odd_over_even": round(odd / even, 4)}
         if name != "valu":
             line["GBps"] = round(need / (statistics.median(r[0] for r in v) * 1e-3) / 1e9, 1)
