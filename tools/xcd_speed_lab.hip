@@ -79,7 +79,67 @@ __global__ __launch_bounds__(64) void k_store_xcd(uint8_t *dst, uint64_t *out, u
     stamp(out, t0);
 }
 
+// the lane pattern with `nap` s_sleep(1) (64 clocks each) after every 32-store burst
+__global__ __launch_bounds__(64) void k_store_lanes_paced(uint8_t *dst, uint64_t *out, uint32_t span, uint32_t units,
+                                                          uint32_t nap) {
+    const uint64_t t0 = wall_clock64();
+    const uint32_t l = threadIdx.x, piece = l % 32;
+    const u32x4 v = {l * 0x01010101u, blockIdx.x, 0xA5A5A5A5u, ~l};
+    for (uint32_t u = 0; u < units; ++u) {
+        uint8_t *base = dst + ((uint64_t)u * gridDim.x + blockIdx.x) * 64ull * span;
+        for (uint32_t it = 0; it < span / 512; ++it) {
+            for (int i = 0; i < 32; ++i) st_sc1(base + (uint64_t)(2 * i + l / 32) * span + it * 512 + piece * 16, v);
+            for (uint32_t n = 0; n < nap; ++n) __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    stamp(out, t0);
+}
+
+// a narrow sliding window: at step j every wave b writes granule j*grid + b,
+// so the resident waves write a window of grid x 4 KiB (4 MiB at 1024 waves)
+// that sweeps the buffer, as the fill's dispatch order does
+__global__ __launch_bounds__(64) void k_store_window(uint8_t *dst, uint64_t *out, uint64_t ngran) {
+    const uint64_t t0 = wall_clock64();
+    const u32x4 v = {threadIdx.x * 0x01010101u, blockIdx.x, 0x69696969u, ~threadIdx.x};
+    for (uint64_t g = blockIdx.x; g < ngran; g += gridDim.x)
+        for (int i = 0; i < 4; ++i) st_sc1(dst + g * 4096 + threadIdx.x * 16 + 1024 * i, v);
+    stamp(out, t0);
+}
+
+// the lane pattern with data that changes every store (a 32-bit LCG per lane)
+__global__ __launch_bounds__(64) void k_store_lanes_rnd(uint8_t *dst, uint64_t *out, uint32_t span, uint32_t units) {
+    const uint64_t t0 = wall_clock64();
+    const uint32_t l = threadIdx.x, piece = l % 32;
+    uint32_t x = l * 2654435761u + blockIdx.x * 40503u + 1u;
+    for (uint32_t u = 0; u < units; ++u) {
+        uint8_t *base = dst + ((uint64_t)u * gridDim.x + blockIdx.x) * 64ull * span;
+        for (uint32_t it = 0; it < span / 512; ++it)
+            for (int i = 0; i < 32; ++i) {
+                x = x * 1664525u + 1013904223u;
+                const u32x4 v = {x, x ^ 0x9E3779B9u, x * 3u, ~x};
+                st_sc1(base + (uint64_t)(2 * i + l / 32) * span + it * 512 + piece * 16, v);
+            }
+    }
+    stamp(out, t0);
+}
+
 extern "C" {
+int lab_store_lanes_rnd(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_lanes_rnd, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out,
+                       span, units);
+    return (int)hipGetLastError();
+}
+int lab_store_window(void *dst, void *out, uint32_t grid, uint64_t ngran, uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_window, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out,
+                       ngran);
+    return (int)hipGetLastError();
+}
+int lab_store_lanes_paced(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t nap,
+                          uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_lanes_paced, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst,
+                       (uint64_t *)out, span, units, nap);
+    return (int)hipGetLastError();
+}
 int lab_store_xcd(void *dst, void *out, uint32_t grid, uint32_t units, uint32_t lds, void *s) {
     hipLaunchKernelGGL(k_store_xcd, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out, units);
     return (int)hipGetLastError();

@@ -35,6 +35,9 @@ def main():
     L.lab_store_seq.argtypes = [vp, vp, u32, u64, u32, u32, vp]
     L.lab_store_lanes.argtypes = [vp, vp, u32, u32, u32, u32, vp]
     L.lab_store_xcd.argtypes = [vp, vp, u32, u32, u32, vp]
+    L.lab_store_lanes_paced.argtypes = [vp, vp, u32, u32, u32, u32, u32, vp]
+    L.lab_store_window.argtypes = [vp, vp, u32, u64, u32, vp]
+    L.lab_store_lanes_rnd.argtypes = [vp, vp, u32, u32, u32, u32, vp]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     span = 16384               # 16 KiB lane regions (the keystream's 2048 draws)
     need = 8 * 4 * cus * 64 * span
@@ -55,6 +58,10 @@ def main():
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh))
         kinds["store_xcd" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_xcd(
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, units, lds, sh))
+        kinds["store_window" + sfx] = (lambda grid=grid, lds=lds: L.lab_store_window(
+            vp(buf.data_ptr()), vp(out.data_ptr()), grid, need // 4096, lds, sh))
+        kinds["store_lanes_rnd" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_lanes_rnd(
+            vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh))
     # LAB_SHORT: the lane pattern as one unit per workgroup over a grid of many
     # (lane region bytes per entry), like the keystream's static grid / the
     # fill's short workgroups, four resident per CU
@@ -65,6 +72,10 @@ def main():
         g = need // (64 * sp)
         kinds[f"store_lanes_short_{sp // 1024}k"] = (lambda g=g, sp=sp: L.lab_store_lanes(
             vp(buf.data_ptr()), vp(out.data_ptr()), g, sp, 1, 40 * 1024, sh))
+    # LAB_NAP: the lane pattern (4 per CU) with s_sleep(1) x nap after each 32-store burst
+    for nap in [int(x) for x in os.environ.get("LAB_NAP", "").split(",") if x]:
+        kinds[f"store_lanes_nap{nap}"] = (lambda nap=nap: L.lab_store_lanes_paced(
+            vp(buf.data_ptr()), vp(out.data_ptr()), 4 * cus, span, 8, nap, 40 * 1024, sh))
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "5"))):
         for name, f in kinds.items():
