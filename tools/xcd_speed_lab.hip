@@ -98,11 +98,13 @@ __global__ __launch_bounds__(64) void k_store_lanes_paced(uint8_t *dst, uint64_t
 // a narrow sliding window: at step j every wave b writes granule j*grid + b,
 // so the resident waves write a window of grid x 4 KiB (4 MiB at 1024 waves)
 // that sweeps the buffer, as the fill's dispatch order does
-__global__ __launch_bounds__(64) void k_store_window(uint8_t *dst, uint64_t *out, uint64_t ngran) {
+__global__ __launch_bounds__(64) void k_store_window(uint8_t *dst, uint64_t *out, uint64_t ngran, uint32_t nap) {
     const uint64_t t0 = wall_clock64();
     const u32x4 v = {threadIdx.x * 0x01010101u, blockIdx.x, 0x69696969u, ~threadIdx.x};
-    for (uint64_t g = blockIdx.x; g < ngran; g += gridDim.x)
+    for (uint64_t g = blockIdx.x; g < ngran; g += gridDim.x) {
         for (int i = 0; i < 4; ++i) st_sc1(dst + g * 4096 + threadIdx.x * 16 + 1024 * i, v);
+        for (uint32_t n = 0; n < nap; ++n) __builtin_amdgcn_s_sleep(1);   // `nap` x 64 clocks per 4 KiB granule
+    }
     stamp(out, t0);
 }
 
@@ -123,15 +125,60 @@ __global__ __launch_bounds__(64) void k_store_lanes_rnd(uint8_t *dst, uint64_t *
     stamp(out, t0);
 }
 
+// one 4 KiB granule per workgroup over a grid of every granule (the fill's
+// dispatch shape without its PRNG, LDS image and base-block loads)
+__global__ __launch_bounds__(64) void k_store_granule(uint8_t *dst, uint64_t *out) {
+    const uint64_t t0 = wall_clock64();
+    const u32x4 v = {threadIdx.x * 0x01010101u, blockIdx.x, 0x96969696u, ~threadIdx.x};
+    const uint64_t g = blockIdx.x;
+    for (int i = 0; i < 4; ++i) st_sc1(dst + g * 4096 + threadIdx.x * 16 + 1024 * i, v);
+    stamp(out, t0);
+}
+
+// the lane pattern with `s_waitcnt vmcnt(N)` after every 32-store burst: at
+// most N stores of the wave left in flight before it goes on (a wave of the
+// fill waits on its base-block loads, and so on its earlier stores, each block)
+template <int N>
+__global__ __launch_bounds__(64) void k_store_lanes_wait(uint8_t *dst, uint64_t *out, uint32_t span, uint32_t units) {
+    const uint64_t t0 = wall_clock64();
+    const uint32_t l = threadIdx.x, piece = l % 32;
+    const u32x4 v = {l * 0x01010101u, blockIdx.x, 0xC3C3C3C3u, ~l};
+    for (uint32_t u = 0; u < units; ++u) {
+        uint8_t *base = dst + ((uint64_t)u * gridDim.x + blockIdx.x) * 64ull * span;
+        for (uint32_t it = 0; it < span / 512; ++it) {
+            for (int i = 0; i < 32; ++i) st_sc1(base + (uint64_t)(2 * i + l / 32) * span + it * 512 + piece * 16, v);
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+        }
+    }
+    stamp(out, t0);
+}
+
 extern "C" {
+int lab_store_lanes_wait(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t n, uint32_t lds,
+                         void *s) {
+    if (n == 0)
+        hipLaunchKernelGGL(k_store_lanes_wait<0>, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst,
+                           (uint64_t *)out, span, units);
+    else if (n == 16)
+        hipLaunchKernelGGL(k_store_lanes_wait<16>, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst,
+                           (uint64_t *)out, span, units);
+    else
+        hipLaunchKernelGGL(k_store_lanes_wait<32>, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst,
+                           (uint64_t *)out, span, units);
+    return (int)hipGetLastError();
+}
+int lab_store_granule(void *dst, void *out, uint32_t grid, uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_granule, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out);
+    return (int)hipGetLastError();
+}
 int lab_store_lanes_rnd(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t lds, void *s) {
     hipLaunchKernelGGL(k_store_lanes_rnd, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out,
                        span, units);
     return (int)hipGetLastError();
 }
-int lab_store_window(void *dst, void *out, uint32_t grid, uint64_t ngran, uint32_t lds, void *s) {
+int lab_store_window(void *dst, void *out, uint32_t grid, uint64_t ngran, uint32_t nap, uint32_t lds, void *s) {
     hipLaunchKernelGGL(k_store_window, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out,
-                       ngran);
+                       ngran, nap);
     return (int)hipGetLastError();
 }
 int lab_store_lanes_paced(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t nap,

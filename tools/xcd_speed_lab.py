@@ -36,7 +36,9 @@ def main():
     L.lab_store_lanes.argtypes = [vp, vp, u32, u32, u32, u32, vp]
     L.lab_store_xcd.argtypes = [vp, vp, u32, u32, u32, vp]
     L.lab_store_lanes_paced.argtypes = [vp, vp, u32, u32, u32, u32, u32, vp]
-    L.lab_store_window.argtypes = [vp, vp, u32, u64, u32, vp]
+    L.lab_store_window.argtypes = [vp, vp, u32, u64, u32, u32, vp]
+    L.lab_store_granule.argtypes = [vp, vp, u32, u32, vp]
+    L.lab_store_lanes_wait.argtypes = [vp, vp, u32, u32, u32, u32, u32, vp]
     L.lab_store_lanes_rnd.argtypes = [vp, vp, u32, u32, u32, u32, vp]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     span = 16384               # 16 KiB lane regions (the keystream's 2048 draws)
@@ -58,8 +60,9 @@ def main():
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh))
         kinds["store_xcd" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_xcd(
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, units, lds, sh))
-        kinds["store_window" + sfx] = (lambda grid=grid, lds=lds: L.lab_store_window(
-            vp(buf.data_ptr()), vp(out.data_ptr()), grid, need // 4096, lds, sh))
+        for wn in [int(x) for x in os.environ.get("LAB_WNAP", "0").split(",")]:
+            kinds["store_window" + sfx + (f"_nap{wn}" if wn else "")] = (lambda grid=grid, lds=lds, wn=wn: L.lab_store_window(
+                vp(buf.data_ptr()), vp(out.data_ptr()), grid, need // 4096, wn, lds, sh))
         kinds["store_lanes_rnd" + sfx] = (lambda grid=grid, units=units, lds=lds: L.lab_store_lanes_rnd(
             vp(buf.data_ptr()), vp(out.data_ptr()), grid, span, units, lds, sh))
     # LAB_SHORT: the lane pattern as one unit per workgroup over a grid of many
@@ -76,6 +79,17 @@ def main():
     for nap in [int(x) for x in os.environ.get("LAB_NAP", "").split(",") if x]:
         kinds[f"store_lanes_nap{nap}"] = (lambda nap=nap: L.lab_store_lanes_paced(
             vp(buf.data_ptr()), vp(out.data_ptr()), 4 * cus, span, 8, nap, 40 * 1024, sh))
+    # LAB_WAIT: the lane pattern (4 per CU) with s_waitcnt vmcnt(N) after each burst
+    for n in [int(x) for x in os.environ.get("LAB_WAIT", "").split(",") if x]:
+        kinds[f"store_lanes_vmcnt{n}"] = (lambda n=n: L.lab_store_lanes_wait(
+            vp(buf.data_ptr()), vp(out.data_ptr()), 4 * cus, span, 8, n, 40 * 1024, sh))
+    # LAB_GRANULE: one granule per workgroup, resident workgroups per CU listed
+    gran = [int(x) for x in os.environ.get("LAB_GRANULE", "").split(",") if x]
+    if gran:
+        out = torch.zeros(3 * (need // 4096), dtype=torch.int64, device="cuda")
+    for wpc in gran:
+        kinds[f"store_granule_{wpc}pcu"] = (lambda wpc=wpc: L.lab_store_granule(
+            vp(buf.data_ptr()), vp(out.data_ptr()), need // 4096, (160 // wpc) * 1024, sh))
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "5"))):
         for name, f in kinds.items():
