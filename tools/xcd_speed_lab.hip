@@ -153,7 +153,57 @@ __global__ __launch_bounds__(64) void k_store_lanes_wait(uint8_t *dst, uint64_t 
     stamp(out, t0);
 }
 
+// one granule per workgroup with part of the fill's work in front of the
+// stores: `work` Xoshiro steps (VALU) and/or (load != 0) the lane's four 16-B
+// pieces of a 4 KiB block read from L2 first, as the fill reads its base block
+__global__ __launch_bounds__(64) void k_store_granule_work(uint8_t *dst, uint64_t *out, const u32x4 *blk, uint32_t work,
+                                                           uint32_t load) {
+    const uint64_t t0 = wall_clock64();
+    u32x4 v = {threadIdx.x * 0x01010101u, blockIdx.x, 0x96969696u, ~threadIdx.x};
+    uint64_t s0 = threadIdx.x + 1, s1 = blockIdx.x * 77 + 3, s2 = 0x9E3779B97F4A7C15ull, s3 = 12345;
+    for (uint32_t i = 0; i < work; ++i) {
+        const uint64_t t = s1 << 17;
+        s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45);
+    }
+    v.x ^= (uint32_t)(s0 + s3);
+    u32x4 b[4] = {v, v, v, v};
+    if (load)
+        for (int i = 0; i < 4; ++i) b[i] = blk[threadIdx.x + 64 * i] ^ v;
+    const uint64_t g = blockIdx.x;
+    for (int i = 0; i < 4; ++i) st_sc1(dst + g * 4096 + threadIdx.x * 16 + 1024 * i, b[i]);
+    stamp(out, t0);
+}
+
+// the lane pattern, each 32-store burst's data XOR-ed with the lane's 16 B of
+// an L2-resident block read just before it (the burst waits for that read)
+__global__ __launch_bounds__(64) void k_store_lanes_load(uint8_t *dst, uint64_t *out, const u32x4 *blk, uint32_t span,
+                                                         uint32_t units) {
+    const uint64_t t0 = wall_clock64();
+    const uint32_t l = threadIdx.x, piece = l % 32;
+    const u32x4 v = {l * 0x01010101u, blockIdx.x, 0xE1E1E1E1u, ~l};
+    for (uint32_t u = 0; u < units; ++u) {
+        uint8_t *base = dst + ((uint64_t)u * gridDim.x + blockIdx.x) * 64ull * span;
+        for (uint32_t it = 0; it < span / 512; ++it) {
+            const u32x4 b = blk[(l + it) & 255] ^ v;
+            for (int i = 0; i < 32; ++i) st_sc1(base + (uint64_t)(2 * i + l / 32) * span + it * 512 + piece * 16, b);
+        }
+    }
+    stamp(out, t0);
+}
+
 extern "C" {
+int lab_store_lanes_load(void *dst, void *out, const void *blk, uint32_t grid, uint32_t span, uint32_t units,
+                         uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_lanes_load, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst, (uint64_t *)out,
+                       (const u32x4 *)blk, span, units);
+    return (int)hipGetLastError();
+}
+int lab_store_granule_work(void *dst, void *out, const void *blk, uint32_t grid, uint32_t work, uint32_t load,
+                           uint32_t lds, void *s) {
+    hipLaunchKernelGGL(k_store_granule_work, dim3(grid), dim3(64), lds, (hipStream_t)s, (uint8_t *)dst,
+                       (uint64_t *)out, (const u32x4 *)blk, work, load);
+    return (int)hipGetLastError();
+}
 int lab_store_lanes_wait(void *dst, void *out, uint32_t grid, uint32_t span, uint32_t units, uint32_t n, uint32_t lds,
                          void *s) {
     if (n == 0)

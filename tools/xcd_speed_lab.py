@@ -39,6 +39,8 @@ def main():
     L.lab_store_window.argtypes = [vp, vp, u32, u64, u32, u32, vp]
     L.lab_store_granule.argtypes = [vp, vp, u32, u32, vp]
     L.lab_store_lanes_wait.argtypes = [vp, vp, u32, u32, u32, u32, u32, vp]
+    L.lab_store_granule_work.argtypes = [vp, vp, vp, u32, u32, u32, u32, vp]
+    L.lab_store_lanes_load.argtypes = [vp, vp, vp, u32, u32, u32, u32, vp]
     L.lab_store_lanes_rnd.argtypes = [vp, vp, u32, u32, u32, u32, vp]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     span = 16384               # 16 KiB lane regions (the keystream's 2048 draws)
@@ -87,9 +89,17 @@ def main():
     gran = [int(x) for x in os.environ.get("LAB_GRANULE", "").split(",") if x]
     if gran:
         out = torch.zeros(3 * (need // 4096), dtype=torch.int64, device="cuda")
+    blk = torch.randint(0, 255, (4096,), dtype=torch.uint8, device="cuda")
+    for wpc in [int(x) for x in os.environ.get("LAB_LLOAD", "").split(",") if x]:   # lane pattern + a read per burst
+        kinds[f"store_lanes_load_{wpc}pcu"] = (lambda wpc=wpc: L.lab_store_lanes_load(
+            vp(buf.data_ptr()), vp(out.data_ptr()), vp(blk.data_ptr()), wpc * cus, span, 32 // wpc, (160 // wpc) * 1024, sh))
+    works = [tuple(int(y) for y in x.split("/")) for x in os.environ.get("LAB_GWORK", "").split(",") if x]
     for wpc in gran:
         kinds[f"store_granule_{wpc}pcu"] = (lambda wpc=wpc: L.lab_store_granule(
             vp(buf.data_ptr()), vp(out.data_ptr()), need // 4096, (160 // wpc) * 1024, sh))
+        for work, load in works:   # LAB_GWORK "steps/load,...": VALU steps and the L2 block read before the stores
+            kinds[f"store_granule_{wpc}pcu_w{work}_l{load}"] = (lambda wpc=wpc, work=work, load=load: L.lab_store_granule_work(
+                vp(buf.data_ptr()), vp(out.data_ptr()), vp(blk.data_ptr()), need // 4096, work, load, (160 // wpc) * 1024, sh))
     res = {}
     for rep in range(int(os.environ.get("LAB_REPS", "5"))):
         for name, f in kinds.items():
