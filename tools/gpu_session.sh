@@ -11,7 +11,7 @@
 #   smoke               __graft_entry__.smoke()
 #   bench:CFG[:ARGS]    bench.py --config CFG --steps 20 --warmup 5 ARGS (':'-separated)
 #   envbench:ENV:CFG    the same with ENV (comma-separated K=V) set
-#   driver              bench.py with no flags (the driver's own command)
+#   driver              bench.py --gpus 1 --steps 20 --warmup 5 (the driver's own command; rounds 2-5 ran bench.py with no flags here, 5 steps)
 #   prof:CFG            rocprofv3 --kernel-trace --stats of bench.py --config CFG
 #   pmc:CFG:COUNTER     one rocprofv3 --pmc pass (WRITE_SIZE or FETCH_SIZE) of bench.py --config CFG
 #   rehearsal           bench.py N=8 (config 2) / N=4 (config 5, --d2h-full) launcher rehearsals on device 0
@@ -53,7 +53,7 @@ for step in "$@"; do
             > "$OUT/$tag.log" 2>&1; rc=$?
         grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
     driver)
-        timeout -k 10 400 python -u bench.py > "$OUT/$tag.log" 2>&1; rc=$?
+        timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/$tag.log" 2>&1; rc=$?
         grep '^{' "$OUT/$tag.log" | tail -1 | cut -c1-600;;
     prof)
         timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/$tag" -o run --output-format csv \
