@@ -166,8 +166,9 @@ def parse():
                         "D2H completion), instead of an 8 GiB sample; reported beside the device-resident value")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-ceiling", action="store_true")
-    p.add_argument("--host-mem", choices=["pageable", "pinned"], default="pageable",
-                   help="host configs (18-22): the caller's buffer is pageable (a reused Vec / bytearray) or pinned")
+    p.add_argument("--host-mem", choices=["pageable", "pinned", "registered"], default="pageable",
+                   help="host configs (18-22): the caller's buffer is pageable (a reused Vec / bytearray), pinned "
+                        "by the library, or pageable and page-locked by s3dg_host_register")
     p.add_argument("--device-override", type=int, default=None,
                    help="rehearsal only: put every rank on this device (e.g. 8 ranks on a 1-GPU box)")
     return p.parse_args()
@@ -287,7 +288,7 @@ def main() -> int:
     if kind in ("stream", "keystream"):
         size = cfg["size"]
         stride = (size + 4095) // 4096 * 4096
-        ring_objs = max(1, min(n_rank, ring_cap // stride))
+        ring_objs = even_ring(n_rank, ring_cap // stride)
         ring = torch.empty(ring_objs * stride, dtype=torch.uint8, device=f"cuda:{dev}")
         base_ptr = int(ring.data_ptr())
         for s0 in range(0, n_rank, ring_objs):
@@ -335,7 +336,7 @@ def main() -> int:
         # the calls come from a native loop (tools/native_loop.c), as the
         # reference's criterion loop calls from Rust; the Python-loop rate is
         # reported beside it (single_call)
-        nl = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libnative_loop.so"))
+        nl = ctypes.CDLL(os.path.join(ROOT, "tools", "_native", "libnative_loop.so"))
         u64, u32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p
         nl.nl_fill_loop.restype = ctypes.c_int
         nl.nl_fill_loop.argtypes = [vp, vp, vp, u64, u64, u64, u32, u32, u64, vp]
@@ -356,7 +357,7 @@ def main() -> int:
         # synchronous host-buffer calls from a native loop; the work runs on
         # the library's host slots (S3DLIO_GPU_DEVICE(S)), timed by wall clock
         size, calls, nthr = cfg["size"], args.objects or cfg["n"], cfg.get("threads", 1)
-        nl = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libnative_loop.so"))
+        nl = ctypes.CDLL(os.path.join(ROOT, "tools", "_native", "libnative_loop.so"))
         u64, vp = ctypes.c_uint64, ctypes.c_void_p
         nl.nl_host_fill_loop.argtypes = [vp, vp, u64, u64, u64, u64]
         nl.nl_threads_gen_loop.argtypes = [vp, ctypes.POINTER(vp), u64, ctypes.c_int, u64, u64, u64]
@@ -397,7 +398,7 @@ def main() -> int:
         step_bytes = calls * nthr * size
     elif kind == "dgen_stream":   # DG1 objects, one launch per ring pass
         size = cfg["size"]
-        ring_objs = max(1, min(n_rank, ring_cap // size))
+        ring_objs = even_ring(n_rank, ring_cap // size)
         ring = torch.empty(ring_objs * size, dtype=torch.uint8, device=f"cuda:{dev}")
         base_ptr = int(ring.data_ptr())
         for s0 in range(0, n_rank, ring_objs):
@@ -547,6 +548,9 @@ def main() -> int:
             d2h["whole_job_GiBps"] = round(cp.sum(d2h["bytes"]) / cp.max(d2h["seconds"]) / GiB, 2)
             d2h["verified_vs_oracle"] = bool(cp.max(0.0 if d2h["verified_vs_oracle"] else 1.0) == 0.0)
 
+    # every rank's object range and device (disjoint ranges: no object written twice)
+    rank_map = cp.gather({"rank": rank, "device": dev, "object_range": [lo, hi]})
+
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -567,7 +571,7 @@ def main() -> int:
                     "kernel": kernel, "launch_shape": launch_shape,
                     "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": algo_per_launch,
-                    "launch_ms_distribution": launch_distribution(kern_ms),
+                    "launch_ms_distribution": launch_distribution(kern_ms, launch_bytes),
                     "source_digest": src_digest, "library_digest": lib_digest}
         if kind in ("stream", "batch"):
             # the zero-class setting the context measured and chose (s3dg_query_zero_tune)
@@ -609,6 +613,7 @@ def main() -> int:
             "cpu_baseline": cpu,
             "d2h_inclusive": d2h,
             "verified_vs_oracle": verified,
+            "ranks": rank_map,
         }
         if single_call:
             out["single_call"] = single_call
@@ -617,19 +622,37 @@ def main() -> int:
     return 0
 
 
-def launch_distribution(ms: list) -> dict:
+def even_ring(n: int, cap_objs: int) -> int:
+    """Objects per ring pass: the fewest passes the ring capacity allows, with
+    the objects spread evenly over them, so every launch of a step writes the
+    same bytes (100 000 objects as 10 x 10 000, not
+    9 x 10 240 + 7 840)."""
+    cap_objs = max(1, min(n, cap_objs))
+    passes = -(-n // cap_objs)
+    return -(-n // passes)
+
+
+def launch_distribution(ms: list, nbytes: list) -> dict:
     """Per-launch HIP-event times of the timed steps (the mean is
     what the line scores, and a bimodal run shows here): mean, p10/p50/p90,
-    max, and the share of launches slower than 1.06 x p10."""
+    max, and per-launch rates (per byte, so launches of
+    different sizes are not mixed) with the share of launches slower than the
+    fast mode, i.e. a rate below p90(rate) / 1.06."""
     v = sorted(ms)
     if not v:
         return {}
 
-    def pct(q):
-        return round(v[min(len(v) - 1, int(q * len(v)))], 4)
-    p10 = v[min(len(v) - 1, int(0.1 * len(v)))]
-    return {"n": len(v), "mean": round(sum(v) / len(v), 4), "p10": pct(0.1), "p50": pct(0.5), "p90": pct(0.9),
-            "max": round(v[-1], 4), "slow_share_over_1.06xp10": round(sum(x > 1.06 * p10 for x in v) / len(v), 4)}
+    def pct(a, q):
+        return round(a[min(len(a) - 1, int(q * len(a)))], 4)
+    rates = sorted(b / (m * 1e6) for m, b in zip(ms, nbytes) if m > 0)
+    fast = rates[min(len(rates) - 1, int(0.9 * len(rates)))] if rates else 0.0
+    out = {"n": len(v), "launch_bytes": sorted(set(int(b) for b in nbytes)), "mean": round(sum(v) / len(v), 4),
+           "p10": pct(v, 0.1), "p50": pct(v, 0.5), "p90": pct(v, 0.9), "max": round(v[-1], 4)}
+    if rates:
+        out.update({"GBps_min": round(rates[0], 1), "GBps_p10": round(pct(rates, 0.1), 1),
+                    "GBps_p50": round(pct(rates, 0.5), 1), "GBps_p90": round(fast, 1),
+                    "slow_share_rate_below_p90_over_1.06": round(sum(r < fast / 1.06 for r in rates) / len(rates), 4)})
+    return out
 
 
 def host_buffer(n: int, kind: str, call):
@@ -642,6 +665,8 @@ def host_buffer(n: int, kind: str, call):
         ctypes.memset(p.value, 1, n)
         return p.value, p
     a = np.ones(n, np.uint8)
+    if kind == "registered":   # a reused pageable buffer the caller page-locks (s3dg_host_register)
+        call("s3dg_host_register", int(a.ctypes.data), n)
     return int(a.ctypes.data), a
 
 

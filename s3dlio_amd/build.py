@@ -90,7 +90,7 @@ def build_bytesview(force: bool = False, verbose: bool = False) -> str:
 
 
 NL_SRC = os.path.join(ROOT, "tools", "native_loop.c")
-NL_LIB = os.path.join(ROOT, "tools", "_build", "libnative_loop.so")
+NL_LIB = os.path.join(ROOT, "tools", "_native", "libnative_loop.so")   # travels to the GPU box (tools/_build does not)
 
 
 def build_native_loop(force: bool = False, verbose: bool = False) -> str:

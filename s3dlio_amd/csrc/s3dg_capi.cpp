@@ -397,8 +397,17 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
     return cand;
 }
 
-// Record the timed launch's events around it (start before, end after).
-void tune_mark(s3dg_ctx *c, int zc, const ZcTuner::Pending &probe, bool end, hipStream_t s) {
+// Record the timed launch's events around it (start before, end after).  A
+// probe whose launch failed (launched = false at the end mark) records no rate:
+// its events go straight back to the spares (its near-zero elapsed
+// time would otherwise enter the medians as a huge GB/s sample).
+void tune_mark(s3dg_ctx *c, int zc, const ZcTuner::Pending &probe, bool end, hipStream_t s, bool launched = true) {
+    if (end && !launched) {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->tune[zc].spare.push_back(probe.a);
+        c->tune[zc].spare.push_back(probe.b);
+        return;
+    }
     (void)hipEventRecord(end ? probe.b : probe.a, s);
     if (end) {
         std::lock_guard<std::mutex> g(c->mu);
@@ -873,7 +882,7 @@ static int fill_uniform(s3dg_ctx *c, uint8_t *dst, uint64_t obj_size, uint64_t s
         if (zc == kZcNone && c->batch_rt_floor < 0 && nb >= kRtFloorLargeBlocks) lc.rt_floor = kRtFloorLargeUniform;
         const hipError_t le = launch_fill_uniform_tiles(lc, dst, obj_size, stride, n_objs, (uint32_t)tpo, tshift, lead,
                                                         seed_base + (first_obj << 32), pp, S->tiles, c->base_dev, s);
-        if (timed) tune_mark(c, zc, probe, true, s);
+        if (timed) tune_mark(c, zc, probe, true, s, le == hipSuccess);
         HIP_TRY(le,
                 "launch k_fill_batch(stream)");
         return S3DG_OK;
@@ -1387,8 +1396,8 @@ int s3dg_fill_controlled_batch(s3dg_ctx *c, void *dst_base, const s3dg_obj_desc 
             le = launch_batch_tiles(lcs, (uint8_t *)dst_base, recs, tshift, S->btiles[tb], c->base_dev, s);
         }
         // the probe's end mark even when a launch failed: its events go back
-        // to the tuner (harvested later) instead of leaking
-        if (timed) tune_mark(c, zcls, probe, true, s);
+        // to the tuner's spares instead of leaking, with no rate
+        if (timed) tune_mark(c, zcls, probe, true, s, le == hipSuccess);
         HIP_TRY(le, "launch k_fill_batch");
         HIP_TRY(hipEventRecord(S->filled[tb], s), "hipEventRecord");
         k0 = k1;
@@ -1603,6 +1612,15 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     if (int r = ks_counters(SL.get(), &kc)) return r;
     hipStream_t s = (hipStream_t)stream;
     StreamState *SS = SL.get();
+    // An error after the side stream's zero launch was queued must not return
+    // while that launch may still write the caller's buffer (the caller's
+    // stream never got to wait on zjoin): drain the side stream first.
+    struct ZeroJoinGuard {
+        hipStream_t zs = nullptr;
+        ~ZeroJoinGuard() {
+            if (zs) (void)hipStreamSynchronize(zs);
+        }
+    } zguard;
     if (zsplit && !overlap) {   // the prefixes' whole granules first (the tail launch masks a partial one)
         HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zw, zlc, s),
                 "launch k_zero_prefix");
@@ -1612,6 +1630,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
             if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
         HIP_TRY(hipEventRecord(SS->zfork, s), "hipEventRecord");
         HIP_TRY(hipStreamWaitEvent(SS->zs, SS->zfork, 0), "hipStreamWaitEvent");
+        zguard.zs = SS->zs;   // from here an error return first drains the side stream
         HIP_TRY(launch_zero_prefix((uint8_t *)dst, nchunks, A.cpo, stride, kDgenBlock, zw, zlc, SS->zs),
                 "launch k_zero_prefix");
         HIP_TRY(hipEventRecord(SS->zjoin, SS->zs), "hipEventRecord");
@@ -1653,6 +1672,7 @@ int s3dg_internal_dgen_chunk(s3dg_ctx *c, void *dst, uint64_t obj_size, uint64_t
     HIP_TRY(launch_keystream((uint8_t *)dst, A, jt, sh, s, kc, c->cus, c->ks_persist, tail ? &A2 : nullptr, jt2),
             "launch k_keystream(dgen)");
     if (zsplit && overlap) HIP_TRY(hipStreamWaitEvent(s, SS->zjoin, 0), "hipStreamWaitEvent");
+    zguard.zs = nullptr;   // joined: the caller's stream now orders after the zero launch
     return S3DG_OK;
 }
 

@@ -27,19 +27,19 @@
 // memory itself); "staged" copies into a pinned bounce buffer of the staging
 // set and from there into the caller's buffer with host threads, overlapped
 // with the next chunk (DESIGN.md §5.8 has the A/B).
-// Registration (S3DLIO_HOST_REGISTER=1, opt-in): a pageable caller buffer
-// seen twice with the same address and length (the criterion loop of
-// benches/performance_microbenchmarks.rs:43-64 reuses one buffer) is
-// page-locked with hipHostRegister and from then on written by the kernel
-// directly, as library-pinned memory.  LIFETIME RULE: such a buffer must stay
-// allocated until s3dg_host_unregister(buf) (or NULL: all) or process exit;
-// freeing it while registered leaves the GPU mapping on the old pages.
+// Registration (s3dg_host_register, explicit): a caller buffer it names is
+// page-locked with hipHostRegister, and calls inside it are written by the
+// kernel directly, as library-pinned memory (the criterion loop of
+// benches/performance_microbenchmarks.rs:43-64 reuses one buffer).  The
+// buffer should stay allocated until s3dg_host_unregister(buf); a call into
+// a registered range whose pages were re-mapped is detected and redone.
 #include "s3dg_internal.h"
 #include "s3dlio_gpu.h"
 
 #include <sys/random.h>
 #include <time.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -441,20 +441,19 @@ int host_launch_blocks(HostStaging *sg, const HostJob &J, uint8_t *dst, uint64_t
     return S3DG_OK;
 }
 
-// ---- opt-in registration of repeated pageable buffers (S3DLIO_HOST_REGISTER=1)
+// ---- explicit registration of caller buffers (s3dg_host_register)
+//
+// Round 5 registered a pageable buffer on its second sighting (env
+// S3DLIO_HOST_REGISTER=1).  That was unsound: a buffer freed and re-allocated
+// at the same address (free + munmap, then mmap; the `b = bytearray(n)` loop)
+// kept the old registration, and the kernel wrote the old pinned pages while
+// the caller's new pages kept their old bytes (ADVICE
+// r05).  Now a buffer is registered only by the caller's own call, and every
+// direct call into a registered range checks that its pages are still the
+// pinned ones (stale_probe below): a stale range is dropped and the call
+// redone through the regular path, so a caller that breaks the lifetime rule
+// still gets the right bytes.
 namespace {
-constexpr int kRegMax = 64;                        // registered ranges at once
-constexpr uint64_t kRegMaxBytes = 4ull << 30;      // registered bytes at once
-constexpr size_t kRegSeenMax = 256;                // remembered (address, length) sightings
-
-bool host_register_on() {
-    static const bool on = [] {
-        const char *v = getenv("S3DLIO_HOST_REGISTER");
-        return v && strcmp(v, "1") == 0;
-    }();
-    return on;
-}
-
 struct UserReg {
     uint64_t bytes;    // page-rounded length
     uint8_t *dev;      // device pointer of the first page
@@ -464,8 +463,8 @@ struct UserRegs {
     std::mutex mu;
     std::condition_variable cv;                      // a registration's users dropped to 0
     std::map<uintptr_t, UserReg> regs;               // page start -> registration
-    std::map<std::pair<uintptr_t, uint64_t>, int> seen;
-    uint64_t bytes = 0;
+    std::atomic<uint64_t> stale{0};                  // registrations found stale and dropped
+    std::atomic<uint64_t> probe_ctr{0};
 };
 UserRegs &userregs() {
     static UserRegs *r = new UserRegs();   // never freed: outlives static teardown
@@ -488,7 +487,6 @@ int drop_regs(UserRegs &R, std::unique_lock<std::mutex> &g, Hit hit) {
             } else {
                 (void)hipHostUnregister((void *)q->first);
                 (void)hipGetLastError();
-                R.bytes -= q->second.bytes;
                 q = R.regs.erase(q);
                 ++dropped;
             }
@@ -499,72 +497,116 @@ int drop_regs(UserRegs &R, std::unique_lock<std::mutex> &g, Hit hit) {
 }
 
 // A host call's hold on a registered range (UserHold::key != 0), released
-// when the call returns.
+// when the call returns (or earlier, by release()).
 struct UserHold {
     uintptr_t key = 0;
-    ~UserHold() {
+    void release() {
         if (!key) return;
         UserRegs &R = userregs();
         std::lock_guard<std::mutex> g(R.mu);
         auto it = R.regs.find(key);
         if (it != R.regs.end() && --it->second.users == 0) R.cv.notify_all();
+        key = 0;
     }
+    ~UserHold() { release(); }
 };
 
-// The device pointer of [p, p+n) when it lies in a registered range; on the
-// second call with this (p, n), registers its pages first (may_register: the
-// call can take the direct path).  A call inside a registered range holds it
-// (hold) until it returns, direct or not, so no other thread unregisters pages
-// it is writing.  A range that overlaps registered ones without lying inside
-// one unregisters them first, once their holders have returned: HIP treats a
-// copy into a partly registered range as pinned and fails (two threads'
-// buffers can share a page).  nullptr: use the regular paths.
-uint8_t *user_registered(const uint8_t *p, uint64_t n, bool may_register, UserHold &hold) {
+// The device pointer of [p, p+n) when it lies inside a registered range; the
+// call then holds that range (hold) until it returns, so no other thread
+// unregisters pages it is writing.  A range that overlaps registered ones
+// without lying inside one unregisters them first, once their holders have
+// returned: HIP treats a copy into a partly registered range as pinned and
+// fails (two buffers can share a page).  nullptr: use the regular paths.
+uint8_t *user_registered(const uint8_t *p, uint64_t n, bool direct_ok, UserHold &hold) {
     UserRegs &R = userregs();
     const uintptr_t a = (uintptr_t)p;
     std::unique_lock<std::mutex> g(R.mu);
+    if (R.regs.empty()) return nullptr;
     auto it = R.regs.upper_bound(a);
     if (it != R.regs.begin()) {
         --it;
         if (a >= it->first && a + n <= it->first + it->second.bytes) {
+            if (!direct_ok) return nullptr;   // inside: the regular paths' copies are valid too
             ++it->second.users;
             hold.key = it->first;
-            return may_register ? it->second.dev + (a - it->first) : nullptr;
+            return it->second.dev + (a - it->first);
         }
     }
     const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
     drop_regs(R, g, [&](uintptr_t s0, uint64_t len) { return s0 < hi && s0 + len > lo; });
-    if (!may_register) return nullptr;
-    if (R.seen.size() >= kRegSeenMax) R.seen.clear();
-    if (++R.seen[{a, n}] < 2) return nullptr;
-    if ((int)R.regs.size() >= kRegMax || R.bytes + (hi - lo) > kRegMaxBytes) return nullptr;
-    if (hipHostRegister((void *)lo, hi - lo, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+    return nullptr;
+}
+
+// Stale-page probe of a direct call into a registered range: before the
+// launch, one word (up to 8 bytes, inside the request) of every 4 KiB page of
+// [buf, buf+n) is set, through the caller's own mapping, to a mark whose bytes
+// are all non-zero; after the kernel, a page whose word still holds the mark
+// was not written through that mapping: the registration's pages are no
+// longer the buffer's.  (Generated bytes equal to the mark, ~2^-64 per page,
+// also read as stale: the call is redone, which is safe.)
+struct StaleProbe {
+    uint64_t mark = 0;
+    void set(uint8_t *buf, uint64_t n) {
+        uint64_t x = userregs().probe_ctr.fetch_add(1, std::memory_order_relaxed) * 0x9E3779B97F4A7C15ull +
+                     0xD1B54A32D192ED03ull;
+        x ^= x >> 31;
+        mark = x | 0x0101010101010101ull;   // no zero byte: zero prefixes never match it
+        walk(buf, n, [&](uint8_t *q, uint64_t k) {
+            memcpy(q, &mark, k);
+            return true;
+        });
+    }
+    bool intact(uint8_t *buf, uint64_t n) const {   // true: every page was written
+        return walk(buf, n, [&](uint8_t *q, uint64_t k) { return memcmp(q, &mark, k) != 0; });
+    }
+    template <class F>
+    static bool walk(uint8_t *buf, uint64_t n, F f) {
+        const uintptr_t a = (uintptr_t)buf, e = a + n;
+        for (uintptr_t q = a; q < e; q = (q & ~(uintptr_t)4095) + 4096) {
+            const uintptr_t pe = (q & ~(uintptr_t)4095) + 4096;
+            const uint64_t k = std::min<uint64_t>(8, std::min<uint64_t>(pe, e) - q);
+            if (!f((uint8_t *)q, k)) return false;
+        }
+        return true;
+    }
+};
+}  // namespace
+
+extern "C" int s3dg_host_register(void *buf, uint64_t len) {
+    if (!buf || len == 0) return s3dg_internal_fail(S3DG_EINVAL, "s3dg_host_register: null buffer or zero length");
+    UserRegs &R = userregs();
+    const uintptr_t a = (uintptr_t)buf;
+    const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + len + 4095) & ~(uintptr_t)4095;
+    std::unique_lock<std::mutex> g(R.mu);
+    auto it = R.regs.find(lo);
+    if (it != R.regs.end() && it->second.bytes == hi - lo) return S3DG_OK;   // already registered
+    drop_regs(R, g, [&](uintptr_t s0, uint64_t l) { return s0 < hi && s0 + l > lo; });
+    hipError_t e = hipHostRegister((void *)lo, hi - lo, hipHostRegisterPortable | hipHostRegisterMapped);
+    if (e != hipSuccess) {
         (void)hipGetLastError();
-        return nullptr;
+        return s3dg_internal_fail(S3DG_EHIP, (std::string("hipHostRegister: ") + hipGetErrorString(e)).c_str());
     }
     void *d = nullptr;
-    if (hipHostGetDevicePointer(&d, (void *)lo, 0) != hipSuccess || !d) {
+    e = hipHostGetDevicePointer(&d, (void *)lo, 0);
+    if (e != hipSuccess || !d) {
         (void)hipGetLastError();
         (void)hipHostUnregister((void *)lo);
-        return nullptr;
+        (void)hipGetLastError();
+        return s3dg_internal_fail(S3DG_EHIP, "hipHostGetDevicePointer failed for a registered buffer");
     }
-    R.regs[lo] = UserReg{hi - lo, (uint8_t *)d, 1};
-    R.bytes += hi - lo;
-    R.seen.erase({a, n});
-    hold.key = lo;
-    return (uint8_t *)d + (a - lo);
+    R.regs[lo] = UserReg{hi - lo, (uint8_t *)d, 0};
+    return S3DG_OK;
 }
-}  // namespace
 
 extern "C" int s3dg_host_unregister(void *buf) {
     UserRegs &R = userregs();
     std::unique_lock<std::mutex> g(R.mu);
     const uintptr_t a = (uintptr_t)buf;
     // waits for calls still writing into a matching range (other threads')
-    const int released = drop_regs(R, g, [&](uintptr_t s0, uint64_t len) { return !buf || (a >= s0 && a < s0 + len); });
-    R.seen.clear();
-    return released;
+    return drop_regs(R, g, [&](uintptr_t s0, uint64_t len) { return !buf || (a >= s0 && a < s0 + len); });
 }
+
+extern "C" uint64_t s3dg_host_register_stale(void) { return userregs().stale.load(); }
 
 // The kernel may write the request's covering blocks straight into `buf`:
 // pinned memory this library allocated, 16-B aligned, and the blocks start
@@ -689,15 +731,31 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
     uint8_t *kdst = buf;
     UserHold hold;   // released on return: the call's copies and kernels are done by then
-    if (!direct && host_register_on()) {
+    StaleProbe probe;
+    bool probed = false;
+    if (!direct) {
         const bool geo = !d2h_staged() && direct_geometry(J, buf, pos, n);
-        if (uint8_t *d = user_registered(buf, n, geo, hold)) {   // a repeated pageable buffer, now page-locked
-            direct = true;
+        if (uint8_t *d = user_registered(buf, n, geo, hold)) {   // inside a caller-registered buffer
+            direct = probed = true;
             kdst = d;
+            probe.set(buf, n);
         }
     }
-    const int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct, kdst)
-                                                                : host_run_chunks(sg, S, J, buf, pos, n);
+    int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct, kdst)
+                                                          : host_run_chunks(sg, S, J, buf, pos, n);
+    if (r == S3DG_OK && probed && !probe.intact(buf, n)) {
+        // the registration's pages are not the buffer's any more (freed and
+        // re-mapped at the same address): drop it and redo the call regularly
+        UserRegs &R = userregs();
+        const uintptr_t key = hold.key;
+        hold.release();
+        {
+            std::unique_lock<std::mutex> g(R.mu);
+            if (drop_regs(R, g, [&](uintptr_t s0, uint64_t) { return s0 == key; }) > 0) ++R.stale;
+        }
+        r = n <= small_max() && !d2h_staged() ? host_run_small(sg, S, J, buf, pos, n, false, buf)
+                                              : host_run_chunks(sg, S, J, buf, pos, n);
+    }
     if (r != S3DG_OK)
         for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);   // nothing lands later
     return r;

@@ -964,7 +964,9 @@ __global__ __launch_bounds__(64 * W) void k_keystream(uint8_t *dst, KeystreamArg
 // (mod 8) in the buffer: every XCD on every 8th granule, as the fill
 // (DESIGN.md §5.1).  The dgen keystream's own all-zero waves write 64 lane
 // regions per wave instead (§5.2).  Chunk y -> object y / cpo by Lemire's
-// fastdiv (m_cpo = floor(2^64 / cpo) + 1; y, cpo < 2^32).
+// fastdiv (m_cpo = floor(2^64 / cpo) + 1; y, cpo < 2^32).  That constant wraps
+// to 0 for cpo == 1 (one chunk per object, e.g. a ragged [0,1) block range), so
+// that case takes ko = y directly (a uniform branch).
 template <int SP, int NW>
 __global__ __launch_bounds__(64 * NW) void k_zero_prefix(uint8_t *dst, uint64_t y0, uint64_t cpo, uint64_t m_cpo,
                                                          uint64_t obj_stride, uint64_t chunk_bytes, uint32_t zw) {
@@ -972,7 +974,7 @@ __global__ __launch_bounds__(64 * NW) void k_zero_prefix(uint8_t *dst, uint64_t 
     if ((uint64_t)x * kBlk >= zw) return;
     const uint32_t lim = zw - x * kBlk;   // bytes of this granule below zw (a multiple of 16)
     const uint64_t y = y0 + blockIdx.y;
-    const uint64_t ko = __umul64hi(m_cpo, y);
+    const uint64_t ko = cpo == 1 ? y : __umul64hi(m_cpo, y);
     const uint64_t cl = y - ko * cpo;
     uint64_t off = ko * obj_stride + cl * chunk_bytes + (uint64_t)x * kBlk;
     asm volatile("" : "+v"(off));   // the address on the VALU

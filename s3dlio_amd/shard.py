@@ -57,6 +57,14 @@ class ControlPlane:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
         return float(t.item())
 
+    def gather(self, obj) -> list:
+        """Every rank's `obj` (a small picklable value), in rank order."""
+        if self.pg is None:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
     def close(self) -> None:
         if self.pg is not None and self.pg.is_initialized():
             self.pg.destroy_process_group()

@@ -156,3 +156,30 @@ def test_ragged_stream_splits_full_blocks(S, oracle, one, gpu_ctx, size, c):
     fn, fd = S.compress_ratio(c)
     exp = oracle.dgen_fill(size, 2, fn, fd, S.object_entropy(sb, 1 + n - 1))
     assert bytes(a[(n - 1) * stride:(n - 1) * stride + size].cpu().numpy()) == bytes(exp)
+
+
+@pytest.mark.parametrize("ctxname", ["gpu_ctx", "split"])
+@pytest.mark.parametrize("c", [2, 3])
+def test_one_full_block_per_object(S, oracle, one, request, ctxname, c):
+    """Objects of 1 MiB + 100 B at a 4 KiB-rounded stride: the full blocks
+    split as one chunk per object (cpo = 1, the zero launch's fastdiv
+    special case), the 100-B tails in a launch of their own.  Equal to the
+    single launch and the oracle, the gaps between objects untouched."""
+    import torch
+    ctx = request.getfixturevalue(ctxname)
+    size, n, sb = MiB + 100, 80, 0x5EED000000000003
+    stride = (size + 4095) // 4096 * 4096
+    a, b = _pair(torch, n * stride)
+    ctx.dgen_fill_stream(a, size, n, stride=stride, dedup=1, compress=c, seed_base=sb, first_obj=2)
+    one.dgen_fill_stream(b, size, n, stride=stride, dedup=1, compress=c, seed_base=sb, first_obj=2)
+    torch.cuda.synchronize()
+    ha = a.cpu().numpy()
+    hb = b.cpu().numpy()
+    fn, fd = S.compress_ratio(c)
+    for j in range(n):
+        o = j * stride
+        assert np.array_equal(ha[o:o + size], hb[o:o + size]), j
+        assert (ha[o + size:o + stride] == 0xAB).all(), j
+    for j in (0, n // 2, n - 1):
+        exp = oracle.dgen_fill(size, 1, fn, fd, S.object_entropy(sb, 2 + j))
+        assert bytes(ha[j * stride:j * stride + size]) == bytes(exp), j

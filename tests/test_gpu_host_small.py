@@ -265,11 +265,11 @@ def test_small_calls_threads(L, oracle, golden_base):
 
 
 def test_registered_pageable_buffer_child(oracle, golden_base):
-    """S3DLIO_HOST_REGISTER=1 (child process): a pageable buffer passed again
-    is page-locked and written by the kernel directly.
-    Every call's bytes equal the oracle's, guard pages around the buffer stay
-    untouched, s3dg_host_unregister reports the registration, and calls after
-    it (and with other lengths inside the buffer) are still exact."""
+    """s3dg_host_register (child process): a registered pageable buffer is
+    written by the kernel directly (made explicit in
+    round 6).  Every call's bytes equal the oracle's, guard pages around the
+    buffer stay untouched, s3dg_host_unregister reports the registration, and
+    calls after it (and with other lengths inside the buffer) are still exact."""
     code = (
         "import ctypes, hashlib, numpy as np, sys; sys.path.insert(0, %r)\n"
         "from s3dlio_amd._lib import lib as L\n"
@@ -279,6 +279,8 @@ def test_registered_pageable_buffer_child(oracle, golden_base):
         "MiB = 1 << 20; g = 8192\n"
         "raw = np.full(3 * MiB + 2 * g + 4096, 0xA5, np.uint8)\n"
         "o = (-raw.ctypes.data) %% 4096 + g\n"
+        "assert L.s3dg_host_register(raw.ctypes.data + o, 3 * MiB) == 0\n"
+        "assert L.s3dg_host_register(raw.ctypes.data + o, 3 * MiB) == 0   # again: no-op\n"
         "def run(size, d, c, ent):\n"
         "    fn, fd = {1: (0, 1), 2: (1, 2), 3: (2, 3)}[c]\n"
         "    assert L.s3dlio_fill_controlled_data_seeded(raw.ctypes.data + o, size, d, c, ent, base) == 0\n"
@@ -288,25 +290,80 @@ def test_registered_pageable_buffer_child(oracle, golden_base):
         "for k in range(5): run(MiB, 1, 1, 100 + k)\n"
         "for k in range(3): run(2 * MiB + 4096, 2, 3, 200 + k)\n"
         "run(MiB - 4096, 3, 2, 300)\n"
-        "n = L.s3dg_host_unregister(None); assert n >= 1, n\n"
+        "assert L.s3dg_host_register_stale() == 0\n"
+        "n = L.s3dg_host_unregister(None); assert n == 1, n\n"
         "for k in range(3): run(3 * MiB, 1, 2, 400 + k)\n"
+        "assert L.s3dg_host_register(raw.ctypes.data + o, 3 * MiB) == 0\n"
+        "run(3 * MiB, 1, 2, 500)\n"
         "assert L.s3dg_host_unregister(ctypes.c_void_p(raw.ctypes.data + o + 5)) == 1\n"
         "assert L.s3dg_host_unregister(None) == 0\n"
         "print('registered ok', n)\n" % (ROOT, os.path.join(ROOT, "tests", "golden", "base_block_ba5eb10c.bin")))
-    env = dict(os.environ, S3DLIO_HOST_REGISTER="1")
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "registered ok" in out.stdout
 
 
+def test_registered_buffer_remapped_child(oracle, golden_base):
+    """The lifetime rule broken (child process): a buffer
+    is registered and filled, then munmap'ed and mmap'ed again at the same
+    address (MAP_FIXED: new pages) without s3dg_host_unregister.  The next
+    calls' bytes must land in the NEW mapping, equal to the oracle (the
+    stale-page probe drops the registration and redoes the call, or the
+    driver's mapping already follows the new pages).  Then the pattern of a
+    Python loop that frees and re-allocates a buffer at the same address."""
+    code = (
+        "import ctypes, numpy as np, sys; sys.path.insert(0, %r)\n"
+        "from s3dlio_amd._lib import lib as L\n"
+        "from oracle import oracle_c as OC\n"
+        "gb = np.frombuffer(open(%r, 'rb').read(), np.uint8)\n"
+        "base = (ctypes.c_uint8 * 4096).from_buffer_copy(gb.tobytes())\n"
+        "libc = ctypes.CDLL(None, use_errno=True)\n"
+        "libc.mmap.restype = ctypes.c_void_p\n"
+        "libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]\n"
+        "libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]\n"
+        "MiB = 1 << 20; N = 2 * MiB\n"
+        "PROT, ANON, FIXED = 3, 0x22, 0x10\n"
+        "p = libc.mmap(None, N, PROT, ANON, -1, 0); assert p not in (None, ctypes.c_void_p(-1).value)\n"
+        "def run(size, c, ent, tag):\n"
+        "    fn, fd = {1: (0, 1), 2: (1, 2), 3: (2, 3)}[c]\n"
+        "    assert L.s3dlio_fill_controlled_data_seeded(p, size, 1, c, ent, base) == 0, tag\n"
+        "    got = ctypes.string_at(p, size)\n"
+        "    assert got == bytes(OC.fill_controlled(size, 1, fn, fd, ent, gb)), tag\n"
+        "assert L.s3dg_host_register(p, N) == 0\n"
+        "run(MiB, 1, 1, 'registered'); run(N, 3, 2, 'registered 2')\n"
+        "for k in range(3):\n"
+        "    assert libc.munmap(p, N) == 0\n"
+        "    q = libc.mmap(p, N, PROT, ANON | FIXED, -1, 0); assert q == p, (q, p)\n"
+        "    ctypes.memset(p, 0x5C, N)\n"
+        "    run(MiB, 1, 10 + k, ('remapped', k)); run(N, 2, 20 + k, ('remapped 2', k))\n"
+        "    assert L.s3dg_host_register(p, N) == 0   # the caller registers its new buffer\n"
+        "    run(MiB, 3, 30 + k, ('re-registered', k))\n"
+        "stale = L.s3dg_host_register_stale()\n"
+        "L.s3dg_host_unregister(None)\n"
+        "for k in range(6):   # b = bytearray(n); register; fill; (no unregister) - freed at the next iteration\n"
+        "    b = bytearray(MiB + 8192); a = ctypes.addressof((ctypes.c_char * len(b)).from_buffer(b))\n"
+        "    o = (-a) %% 4096\n"
+        "    assert L.s3dg_host_register(a + o, MiB) == 0\n"
+        "    assert L.s3dlio_fill_controlled_data_seeded(a + o, MiB, 1, 1, 40 + k, base) == 0\n"
+        "    assert bytes(b[o:o + MiB]) == bytes(OC.fill_controlled(MiB, 1, 0, 1, 40 + k, gb)), k\n"
+        "    del b\n"
+        "L.s3dg_host_unregister(None)\n"
+        "print('remapped ok stale=%%d' %% stale)\n" % (ROOT, os.path.join(ROOT, "tests", "golden", "base_block_ba5eb10c.bin")))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "remapped ok" in out.stdout
+    print(out.stdout.strip())
+
+
 def test_registered_buffers_sharing_a_page_child(oracle, golden_base):
-    """S3DLIO_HOST_REGISTER=1 (child process), four threads whose buffers share
+    """s3dg_host_register (child process), four threads whose buffers share
     their boundary pages (one array cut at offsets that are not page
-    multiples), each calling fill_controlled_data on its own buffer eight
-    times: registering one thread's pages would drop a neighbour's overlapping
-    registration, so a call holds its registered range until it returns and an
-    overlapping call waits for it.  Every call's bytes equal the oracle's and
-    nothing outside the buffers changes."""
+    multiples), each registering its own buffer and calling
+    fill_controlled_data on it eight times: registering one thread's pages
+    drops a neighbour's overlapping registration, so a call holds its
+    registered range until it returns and an overlapping registration or call
+    waits for it.  Every call's bytes equal the oracle's and nothing outside
+    the buffers changes."""
     code = (
         "import ctypes, threading, numpy as np, sys; sys.path.insert(0, %r)\n"
         "from s3dlio_amd._lib import lib as L\n"
@@ -324,6 +381,7 @@ def test_registered_buffers_sharing_a_page_child(oracle, golden_base):
         "    try:\n"
         "        o = o0 + t * size\n"
         "        for k in range(8):\n"
+        "            if k %% 3 == 0: assert L.s3dg_host_register(raw.ctypes.data + o, size) == 0\n"
         "            assert L.s3dlio_fill_controlled_data_seeded(raw.ctypes.data + o, size, 1, 1, 1000 * t + k, base) == 0\n"
         "            assert bytes(raw[o:o + size]) == exp[(t, k)], (t, k)\n"
         "    except Exception as e:\n"
@@ -332,9 +390,9 @@ def test_registered_buffers_sharing_a_page_child(oracle, golden_base):
         "[x.start() for x in ts]; [x.join() for x in ts]\n"
         "assert not errs, errs\n"
         "assert (raw[:o0] == 0xA5).all() and (raw[o0 + T * size:] == 0xA5).all()\n"
+        "assert L.s3dg_host_register_stale() == 0\n"
         "L.s3dg_host_unregister(None)\n"
         "print('shared pages ok')\n" % (ROOT, os.path.join(ROOT, "tests", "golden", "base_block_ba5eb10c.bin")))
-    env = dict(os.environ, S3DLIO_HOST_REGISTER="1")
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "shared pages ok" in out.stdout

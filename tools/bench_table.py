@@ -20,6 +20,6 @@ for path in sys.argv[1:]:
         print(" | ".join(str(x) for x in [
             path.split("/")[-1], d["config"]["workload"][:70], d["value"], r.get("achieved"), r.get("frac"),
             round(tr / algo, 5) if tr and algo else None,
-            f'{dist.get("mean")}/{dist.get("p10")}/{dist.get("p90")} slow {dist.get("slow_share_over_1.06xp10")}',
+            f'{dist.get("mean")}/{dist.get("p10")}/{dist.get("p90")} slow {dist.get("slow_share_rate_below_p90_over_1.06")}',
             d2h.get("whole_job_GiBps") or d2h.get("value"), cpu.get("value"), d.get("verified_vs_oracle"),
             r.get("library_digest")]))

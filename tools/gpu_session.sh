@@ -14,6 +14,7 @@
 #   driver              bench.py --gpus 1 --steps 20 --warmup 5 (the driver's own command; rounds 2-5 ran bench.py with no flags here, 5 steps)
 #   prof:CFG            rocprofv3 --kernel-trace --stats of bench.py --config CFG
 #   pmc:CFG:COUNTER     one rocprofv3 --pmc pass (WRITE_SIZE or FETCH_SIZE) of bench.py --config CFG
+#   pmcx:SCRIPT:CTRS    one rocprofv3 --pmc pass of per-XCC counters (tools/xcc_counters.yaml) over tools/SCRIPT
 #   rehearsal           bench.py N=8 (config 2) / N=4 (config 5, --d2h-full) launcher rehearsals on device 0
 #   soak[:N]            tests/test_gpu_fuzz.py with S3DG_FUZZ_SOAK=N (default 15)
 #   lab:SCRIPT[:ENV]    python tools/SCRIPT with ENV (comma-separated K=V) set
@@ -64,6 +65,11 @@ for step in "$@"; do
         timeout -s KILL 240 rocprofv3 --pmc "$b" -d "$OUT/$tag" -o run --output-format csv \
             -- python3 bench.py --config "$a" --steps 3 --warmup 1 --no-ceiling --no-d2h --no-cpu-baseline \
             --no-verify > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -1 "$OUT/$tag.log";;
+    pmcx)           # per-XCC counters (tools/xcc_counters.yaml) over a lab script: pmcx:SCRIPT:C1,C2,...
+        ctrs=$(echo "$b" | tr ',' ' ')
+        timeout -s KILL 120 rocprofv3 -E tools/xcc_counters.yaml --pmc $ctrs -d "$OUT/$tag" -o run \
+            --output-format csv -- python3 "tools/$a" > "$OUT/$tag.log" 2>&1; rc=$?
         tail -1 "$OUT/$tag.log";;
     rehearsal)      # N=8 / N=4 launcher rehearsals, every rank on device 0 (not a scaling measurement)
         timeout -k 10 300 python bench.py --gpus 8 --device-override 0 --objects 64 --config 2 --steps 3 \
