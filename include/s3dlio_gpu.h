@@ -272,22 +272,22 @@ int s3dg_host_free_pinned(void *p);
  * and the other host entry points; whole 4 KiB blocks, 16-byte aligned, up to
  * 16 MiB) are written by the kernel directly, as s3dg_host_alloc_pinned memory
  * (1 MiB: ~33 us against ~57 us through the bounce path).  Registrations that
- * overlap the range are dropped first.  Registering the same range again is a
- * no-op.  Release with s3dg_host_unregister before freeing the buffer.  A call
- * into a registered range whose pages were freed and re-mapped at the same
- * address (the lifetime rule broken) is detected by a per-page probe, the
- * registration dropped and the call redone through the regular path: the
- * bytes are always the caller's.  0 or a negative S3DG_E* status.
- * Replaces round 5's S3DLIO_HOST_REGISTER=1 sighting rule, which could write
- * stale pages. */
+ * overlap the range are dropped first; registering the same range again is a
+ * no-op.  0 or a negative S3DG_E* status.
+ * CONTRACT (hipHostRegister's): the buffer stays allocated until
+ * s3dg_host_unregister.  Unmapped while registered, its GPU mapping goes with
+ * its pages and the next call into it is a GPU memory fault.  The bindings
+ * hold the buffer for the registration's lifetime (Python:
+ * s3dlio_amd.register_host_buffer keeps an export of it; Rust:
+ * HostRegistration<'a> borrows the slice).
+ * Replaces round 5's S3DLIO_HOST_REGISTER=1 sighting rule, which registered
+ * buffers their owners did not know about. */
 int s3dg_host_register(void *buf, uint64_t len);
 /* Release the registration holding `buf` (NULL: every registration), after
  * calls still writing into it return.  Returns the number released (>= 0).
  * A call whose range overlaps a registration without lying inside it also
  * releases that registration (HIP cannot copy into a partly registered range). */
 int s3dg_host_unregister(void *buf);
-/* Registrations found stale (re-mapped pages) and dropped so far. */
-uint64_t s3dg_host_register_stale(void);
 /* NUMA node of `device` from sysfs (-1 when unknown). */
 int s3dg_device_numa_node(int device, int *node);
 int s3dg_d2h_async(s3dg_ctx *ctx, void *host, const void *dev, uint64_t len, void *stream);

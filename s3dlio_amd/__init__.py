@@ -10,8 +10,8 @@ from .hostbuf import BytesView  # noqa: F401
 from .device import (BLOCK_SIZE, DEFAULT_BASE_SEED, Context, compress_ratio,  # noqa: F401
                      device_count, host_context, host_slots, object_entropy, parse_devices,
                      unique_blocks, xoshiro_jump)
-from .data_gen import (fill_controlled_data, fill_controlled_data_seeded, register_host_buffer,  # noqa: F401
-                       unregister_host_buffer)
+from .data_gen import (HostRegistration, fill_controlled_data, fill_controlled_data_seeded,  # noqa: F401
+                       register_host_buffer, unregister_host_buffer)
 from .datagen import (DataGenerator, Generator, ObjectGen, default_data_gen_threads,  # noqa: F401
                       generate_controlled_data_alt, generate_controlled_data_streaming,
                       generate_data, generate_data_with_threads, generate_into_buffer,

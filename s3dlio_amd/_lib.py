@@ -127,7 +127,6 @@ SIGNATURES = {
     "s3dg_host_free_pinned": (c_int, [c_vp]),
     "s3dg_host_register": (c_int, [c_vp, c_u64]),
     "s3dg_host_unregister": (c_int, [c_vp]),
-    "s3dg_host_register_stale": (c_u64, []),
     "s3dg_host_alloc_pinned_local": (c_int, [c_int, c_u64, ctypes.POINTER(c_vp)]),
     "s3dg_device_numa_node": (c_int, [c_int, ctypes.POINTER(c_int)]),
     "s3dg_d2h_async": (c_int, [c_vp, c_vp, c_vp, c_u64, c_vp]),

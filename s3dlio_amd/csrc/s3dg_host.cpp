@@ -31,8 +31,9 @@
 // page-locked with hipHostRegister, and calls inside it are written by the
 // kernel directly, as library-pinned memory (the criterion loop of
 // benches/performance_microbenchmarks.rs:43-64 reuses one buffer).  The
-// buffer should stay allocated until s3dg_host_unregister(buf); a call into
-// a registered range whose pages were re-mapped is detected and redone.
+// buffer must stay allocated until s3dg_host_unregister(buf) (the bindings
+// hold it: s3dlio_amd.register_host_buffer, HostRegistration in the Rust
+// patch).
 #include "s3dg_internal.h"
 #include "s3dlio_gpu.h"
 
@@ -444,15 +445,17 @@ int host_launch_blocks(HostStaging *sg, const HostJob &J, uint8_t *dst, uint64_t
 // ---- explicit registration of caller buffers (s3dg_host_register)
 //
 // Round 5 registered a pageable buffer on its second sighting (env
-// S3DLIO_HOST_REGISTER=1).  That was unsound: a buffer freed and re-allocated
-// at the same address (free + munmap, then mmap; the `b = bytearray(n)` loop)
-// kept the old registration, and the kernel wrote the old pinned pages while
-// the caller's new pages kept their old bytes (ADVICE
-// r05).  Now a buffer is registered only by the caller's own call, and every
-// direct call into a registered range checks that its pages are still the
-// pinned ones (stale_probe below): a stale range is dropped and the call
-// redone through the regular path, so a caller that breaks the lifetime rule
-// still gets the right bytes.
+// S3DLIO_HOST_REGISTER=1).  That was unsound: a caller that frees a buffer
+// never learns that it was registered, and a buffer freed and re-mapped at the
+// same address kept the registration.  On
+// ROCm the driver drops a registered range's GPU mapping when its pages are
+// unmapped, so the next kernel store into it is a GPU memory fault (measured
+// round 6: munmap + mmap(MAP_FIXED) + a call = "illegal memory access"); no
+// check the host can make before a launch sees that.  So a buffer is
+// registered only by the caller's own call, with hipHostRegister's contract:
+// it stays allocated until s3dg_host_unregister.  The bindings enforce that
+// lifetime: the Python handle holds an export of the buffer (it cannot be
+// freed while registered), the Rust guard borrows the slice.
 namespace {
 struct UserReg {
     uint64_t bytes;    // page-rounded length
@@ -463,8 +466,6 @@ struct UserRegs {
     std::mutex mu;
     std::condition_variable cv;                      // a registration's users dropped to 0
     std::map<uintptr_t, UserReg> regs;               // page start -> registration
-    std::atomic<uint64_t> stale{0};                  // registrations found stale and dropped
-    std::atomic<uint64_t> probe_ctr{0};
 };
 UserRegs &userregs() {
     static UserRegs *r = new UserRegs();   // never freed: outlives static teardown
@@ -537,39 +538,6 @@ uint8_t *user_registered(const uint8_t *p, uint64_t n, bool direct_ok, UserHold 
     return nullptr;
 }
 
-// Stale-page probe of a direct call into a registered range: before the
-// launch, one word (up to 8 bytes, inside the request) of every 4 KiB page of
-// [buf, buf+n) is set, through the caller's own mapping, to a mark whose bytes
-// are all non-zero; after the kernel, a page whose word still holds the mark
-// was not written through that mapping: the registration's pages are no
-// longer the buffer's.  (Generated bytes equal to the mark, ~2^-64 per page,
-// also read as stale: the call is redone, which is safe.)
-struct StaleProbe {
-    uint64_t mark = 0;
-    void set(uint8_t *buf, uint64_t n) {
-        uint64_t x = userregs().probe_ctr.fetch_add(1, std::memory_order_relaxed) * 0x9E3779B97F4A7C15ull +
-                     0xD1B54A32D192ED03ull;
-        x ^= x >> 31;
-        mark = x | 0x0101010101010101ull;   // no zero byte: zero prefixes never match it
-        walk(buf, n, [&](uint8_t *q, uint64_t k) {
-            memcpy(q, &mark, k);
-            return true;
-        });
-    }
-    bool intact(uint8_t *buf, uint64_t n) const {   // true: every page was written
-        return walk(buf, n, [&](uint8_t *q, uint64_t k) { return memcmp(q, &mark, k) != 0; });
-    }
-    template <class F>
-    static bool walk(uint8_t *buf, uint64_t n, F f) {
-        const uintptr_t a = (uintptr_t)buf, e = a + n;
-        for (uintptr_t q = a; q < e; q = (q & ~(uintptr_t)4095) + 4096) {
-            const uintptr_t pe = (q & ~(uintptr_t)4095) + 4096;
-            const uint64_t k = std::min<uint64_t>(8, std::min<uint64_t>(pe, e) - q);
-            if (!f((uint8_t *)q, k)) return false;
-        }
-        return true;
-    }
-};
 }  // namespace
 
 extern "C" int s3dg_host_register(void *buf, uint64_t len) {
@@ -605,8 +573,6 @@ extern "C" int s3dg_host_unregister(void *buf) {
     // waits for calls still writing into a matching range (other threads')
     return drop_regs(R, g, [&](uintptr_t s0, uint64_t len) { return !buf || (a >= s0 && a < s0 + len); });
 }
-
-extern "C" uint64_t s3dg_host_register_stale(void) { return userregs().stale.load(); }
 
 // The kernel may write the request's covering blocks straight into `buf`:
 // pinned memory this library allocated, 16-B aligned, and the blocks start
@@ -731,31 +697,15 @@ int host_run(HostStaging *sg, const HostJob &J, uint8_t *buf, uint64_t pos, uint
     bool direct = !d2h_staged() && direct_target(J, buf, pos, n);
     uint8_t *kdst = buf;
     UserHold hold;   // released on return: the call's copies and kernels are done by then
-    StaleProbe probe;
-    bool probed = false;
     if (!direct) {
         const bool geo = !d2h_staged() && direct_geometry(J, buf, pos, n);
         if (uint8_t *d = user_registered(buf, n, geo, hold)) {   // inside a caller-registered buffer
-            direct = probed = true;
+            direct = true;
             kdst = d;
-            probe.set(buf, n);
         }
     }
-    int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct, kdst)
-                                                          : host_run_chunks(sg, S, J, buf, pos, n);
-    if (r == S3DG_OK && probed && !probe.intact(buf, n)) {
-        // the registration's pages are not the buffer's any more (freed and
-        // re-mapped at the same address): drop it and redo the call regularly
-        UserRegs &R = userregs();
-        const uintptr_t key = hold.key;
-        hold.release();
-        {
-            std::unique_lock<std::mutex> g(R.mu);
-            if (drop_regs(R, g, [&](uintptr_t s0, uint64_t) { return s0 == key; }) > 0) ++R.stale;
-        }
-        r = n <= small_max() && !d2h_staged() ? host_run_small(sg, S, J, buf, pos, n, false, buf)
-                                              : host_run_chunks(sg, S, J, buf, pos, n);
-    }
+    const int r = direct || (n <= small_max() && !d2h_staged()) ? host_run_small(sg, S, J, buf, pos, n, direct, kdst)
+                                                                : host_run_chunks(sg, S, J, buf, pos, n);
     if (r != S3DG_OK)
         for (int q = 0; q < 2; ++q) (void)hipStreamSynchronize(sg->st[q]);   // nothing lands later
     return r;
