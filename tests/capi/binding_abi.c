@@ -56,6 +56,20 @@ int main(int argc, char **argv) {
         CHECK("fill_controlled_data_seeded(base) == oracle", memcmp(a, b, n) == 0);
         free(a); free(b);
     }
+    /* HostRegistration (register, fill through the guard's slice, drop = unregister) */
+    {
+        const uint64_t n = 1 * MiB;
+        uint8_t *a = xalloc(n), *b = xalloc(n);
+        CHECK("HostRegistration::new", s3dg_host_register(a, n) == 0);
+        for (int k = 0; k < 3; ++k) {
+            CHECK("fill_controlled_data_seeded(registered)",
+                  s3dlio_fill_controlled_data_seeded(a, n, 1, 1, 77 + (uint64_t)k, NULL) == 0);
+            s3dgo_fill_controlled(b, n, 1, 0, 1, 77 + (uint64_t)k, base);
+            CHECK("fill_controlled_data_seeded(registered) == oracle", memcmp(a, b, n) == 0);
+        }
+        CHECK("HostRegistration drop", s3dg_host_unregister(a) == 1);
+        free(a); free(b);   /* after the unregister: the contract */
+    }
     /* fill_controlled_data (src/data_gen.rs:151): in place, time entropy */
     {
         const uint64_t n = 2 * MiB;
