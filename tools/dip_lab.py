@@ -11,7 +11,7 @@ the fastest setting's p10, and the amdsmi power, GFX clock and PPT residency
 during its blocks.
 
     python tools/dip_lab.py        # GPU box; LAB_SETTINGS "name=pace/occ;...",
-                                   # LAB_POINT cfg2 (default) | cfg3 | cfg4 | cfg8
+                                   # LAB_POINT cfg2 (default) | cfg3 | cfg4 | cfg5 | cfg8
 Tooling only: nothing in the product imports this."""
 import ctypes, json, os, statistics, sys, threading, time
 
@@ -20,6 +20,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 MiB = 1 << 20
 DEFAULT = "plain=-1/-1;pace20=20/-1;pace50=50/-1;pace100=100/-1;occ30=-1/30;occ28=-1/28"
+# config 5 (d2 c3, the mid-line class): the library default (the tuner's pick
+# of floor 100 or plain), each setting forced, and the cap without the floor
+DEFAULT_CFG5 = "default=-1/-1;plain=0/-1;pace100=100/-1;pace150=150/-1;pace200=200/-1;cap29=0/29"
 
 
 def main():
@@ -33,7 +36,8 @@ def main():
     sh = vp(st.cuda_stream)
     p = vp(buf.data_ptr())
     ctxs = {}
-    for item in os.environ.get("LAB_SETTINGS", DEFAULT).split(";"):
+    point = os.environ.get("LAB_POINT", "cfg2")
+    for item in os.environ.get("LAB_SETTINGS", DEFAULT_CFG5 if point == "cfg5" else DEFAULT).split(";"):
         name, _, spec = item.partition("=")
         pace, occ = (int(x) for x in spec.split("/"))
         h = vp()
@@ -44,7 +48,6 @@ def main():
             assert lib.s3dg_set_occupancy(h, -1, occ) == 0
         ctxs[name] = h
 
-    point = os.environ.get("LAB_POINT", "cfg2")
     work = 8 * MiB * n
     if point == "cfg4":      # BASELINE config 4: 10 000 log-uniform objects, d2 c1.5, batch API
         from bench import log_uniform_sizes
@@ -63,6 +66,9 @@ def main():
                                                 u32(1), u64(0x5EED000000000001), u64(0), sh)
         elif point == "cfg4":
             r = lib.s3dg_fill_controlled_batch(h, p, arr, u64(n), sh)
+        elif point == "cfg5":  # config 5's launch shape: 10 000 x 8 MiB, d2 c3
+            r = lib.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(2), u32(2), u32(3),
+                                                u64(0x5EED000000000001), u64(0), sh)
         elif point == "cfg3":  # config 3: 10 000 x 8 MiB, d4 c2
             r = lib.s3dg_fill_controlled_stream(h, p, u64(8 * MiB), u64(8 * MiB), u64(n), u64(4), u32(1), u32(2),
                                                 u64(0x5EED000000000001), u64(0), sh)

@@ -18,6 +18,7 @@
 #   rehearsal           bench.py N=8 (config 2) / N=4 (config 5, --d2h-full) launcher rehearsals on device 0
 #   soak[:N]            tests/test_gpu_fuzz.py with S3DG_FUZZ_SOAK=N (default 15)
 #   lab:SCRIPT[:ENV]    python tools/SCRIPT with ENV (comma-separated K=V) set
+#   exe:PATH            a native program built in this tree (tools/_native/...)
 # Environment: STEPS (bench steps, default 20), WARMUP (default 5).
 set -o pipefail
 OUT=gpurun_out/${1:?out dir}
@@ -71,6 +72,9 @@ for step in "$@"; do
         timeout -s KILL 120 rocprofv3 -E tools/xcc_counters.yaml --pmc $ctrs -d "$OUT/$tag" -o run \
             --output-format csv -- python3 "tools/$a" > "$OUT/$tag.log" 2>&1; rc=$?
         tail -1 "$OUT/$tag.log";;
+    exe)            # a native program built here (e.g. tools/_native/dispatch_lab)
+        timeout -k 10 300 "$a" > "$OUT/$tag.log" 2>&1; rc=$?
+        tail -12 "$OUT/$tag.log";;
     rehearsal)      # N=8 / N=4 launcher rehearsals, every rank on device 0 (not a scaling measurement)
         timeout -k 10 300 python bench.py --gpus 8 --device-override 0 --objects 64 --config 2 --steps 3 \
             --warmup 1 --no-ceiling > "$OUT/${tag}_n8_cfg2.log" 2>&1 && \
