@@ -157,8 +157,9 @@ def parse():
                    help="batch kernel wall-clock store floor in 10-ns ticks (0 = off; default: per launch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-pin", action="store_true",
-                   help="bind the CPU baseline's threads to the cgroup's share of CPUs (GPU-local first)")
+    p.add_argument("--cpu-no-pin", action="store_true",
+                   help="leave the CPU baseline's threads to the scheduler (default: bound to the cgroup's share of "
+                        "CPUs, GPU-local and idlest first)")
     p.add_argument("--no-d2h", action="store_true")
     p.add_argument("--d2h-reps", type=int, default=1, help="D2H-inclusive samples (diagnosis of run-to-run spread)")
     p.add_argument("--d2h-full", action="store_true",
@@ -554,7 +555,7 @@ def main() -> int:
     # ---- CPU baseline (rank 0, N=1 only) ------------------------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes, dev=dev, pin=args.cpu_pin)
+        cpu = cpu_baseline(cfg, fn, fd, args.cpu_seconds, sizes, dev=dev, pin=not args.cpu_no_pin)
 
     if rank == 0:
         if kind == "host":
@@ -963,8 +964,30 @@ def object_entropy_py(seed_base: int, j: int) -> int:
     return (seed_base + (j << 32)) & (2**64 - 1)
 
 
+def cpu_idle_fractions(window: float = 0.25) -> dict:
+    """Per-CPU idle share over `window` seconds (/proc/stat idle + iowait)."""
+    def snap():
+        out = {}
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3].isdigit():
+                f = line.split()
+                v = [int(x) for x in f[1:]]
+                out[int(f[0][3:])] = (v[3] + v[4], sum(v))
+        return out
+    try:
+        a = snap()
+        time.sleep(window)
+        b = snap()
+    except Exception:
+        return {}
+    return {c: (b[c][0] - a[c][0]) / max(1, b[c][1] - a[c][1]) for c in a if c in b}
+
+
 def pin_cpus(dev: int, n: int) -> list[int]:
-    """n CPUs of this process's affinity, those on the GPU's NUMA node first."""
+    """n CPUs of this process's affinity: those on the GPU's NUMA node first,
+    and within each group the ones idlest right now (/proc/stat over 0.25 s),
+    so a baseline pinned on a shared host does not land on CPUs other jobs
+    are busy on (VERDICT r05 next #6)."""
     aff = sorted(os.sched_getaffinity(0))
     local = []
     try:
@@ -979,19 +1002,22 @@ def pin_cpus(dev: int, n: int) -> list[int]:
             local = [c for c in aff if c in ids]
     except Exception:
         local = []
-    return (local + [c for c in aff if c not in local])[:n]
+    idle = cpu_idle_fractions()
+    key = lambda c: -idle.get(c, 0.0)  # noqa: E731
+    return (sorted(local, key=key) + sorted((c for c in aff if c not in local), key=key))[:n]
 
 
-def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=False):
+def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=True):
     """The C restatement of the same generator (oracle, kind 'port') on this
     host's cores, parallel like the reference's Rayon loops: a warm-up sample,
     then `reps` samples of seconds/reps each, the median reported with min and
-    max.  pin: threads bound to the cgroup's share of
-    CPUs, those on the GPU's NUMA node first (threads inherit the calling
-    thread's affinity); off by default: on the shared 256-CPU host a pinned
-    set shares its CPUs with other jobs' threads, and the samples spread
-    10-400 % (profiles/r04/bench/d_*), where the scheduler left free to
-    migrate keeps them within a few per cent."""
+    max.  pin (default since round 6, VERDICT r05 next
+    #6): threads bound to the cgroup's share of CPUs, those on the GPU's NUMA
+    node first and the idlest ones at the time (threads inherit the calling
+    thread's affinity; the sample's buffers are first touched by the pinned
+    thread, so they sit on that node).  Round 4 pinned to the first CPUs of
+    the affinity list and its samples spread 10-400 % on the shared 256-CPU
+    host (profiles/r04/bench/d_*), where others' jobs ran on them."""
     share = cpu_share()
     cpus = pin_cpus(dev, share["threads"]) if pin else None
     saved = os.sched_getaffinity(0)
@@ -1015,7 +1041,8 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=False):
                min_med_max_GiBps=[vals[0], med, vals[-1]], q1_q3_GiBps=[q1, q3],
                spread=round((vals[-1] - vals[0]) / med, 4) if med else None,
                iqr_spread=round((q3 - q1) / med, 4) if med else None,
-               pinned_cpus=f"{len(cpus)} CPUs: {cpus[0]}-{cpus[-1]}" if cpus else "no (scheduler's choice)",
+               pinned_cpus=(f"{len(cpus)} CPUs: " + ",".join(str(c) for c in sorted(cpus))) if cpus
+               else "no (scheduler's choice)",
                sample=f"median of {reps} samples; one sample: " + out["sample"])
     return out
 
