@@ -269,6 +269,10 @@ def main() -> int:
         ctx.set_batch_tile(args.batch_tile)
     if args.pace is not None:
         ctx.set_batch_pace(args.pace)
+    # every launch on a (non-blocking) stream of torch's pool, not the legacy
+    # default stream, whose launches HIP orders against every blocking stream
+    # (the single-call configs 11-13 paid ~0.8 us per call for it)
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     fn, fd = compress_ratio(cfg["compress"])
@@ -1044,6 +1048,13 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=True):
                pinned_cpus=(f"{len(cpus)} CPUs: " + ",".join(str(c) for c in sorted(cpus))) if cpus
                else "no (scheduler's choice)",
                sample=f"median of {reps} samples; one sample: " + out["sample"])
+    if cpus:
+        # beside it, three samples left to the scheduler (the reference's Rayon
+        # pool is not pinned): the pinned median is the reported value, this
+        # shows what pinning costs or gains on the box
+        _cpu_sample(cfg, fn, fd, min(1.0, seconds / reps), sizes, share)
+        un = sorted(_cpu_sample(cfg, fn, fd, seconds / reps, sizes, share)["value"] for _ in range(3))
+        out["unpinned_min_med_max_GiBps"] = [un[0], un[1], un[2]]
     return out
 
 

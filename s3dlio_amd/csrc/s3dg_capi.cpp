@@ -78,24 +78,33 @@ enum ZeroClass { kZcNone = 0, kZcLines = 1, kZcMidHeavy = 2 };
 // differs between boxes.  So a context times its own large launches of that
 // class (HIP events around the fill, read back without waiting, at a later
 // launch) and runs the floor or the plain uncapped launch, whichever wrote
-// faster: after kTuneFirst launches of each (alternating; a process's first
-// launch is slow), the medians of each one's last kTuneKeep rates, the plain
-// launch taken only when it beats the current choice's median by more than
-// kTuneMargin (the class setting otherwise), so two candidates within the
-// noise of each other do not flip from run to run (the
-// best-of-3 rule did); the loser is probed again every kTuneReprobe launches.
+// faster: after kTuneFirst launches of each (alternating; the context's first
+// timed launch is a warm-up and is not sampled), the MEANS of each one's last
+// kTuneKeep rates, the plain launch taken only when it beats the current
+// choice's mean by more than kTuneMargin (the class setting otherwise), so two
+// candidates within the noise of each other do not flip from run to run
+// (the best-of-3 rule did).  Means, not medians (round
+// 6): on a box with the slow mode 47 % of plain config-5 launches ran 12.1-12.8
+// ms against 11.0-11.3, which a median of five does not see, so the tuner kept
+// probing a candidate 4 % slower by mean (tools/dip_lab.py,
+// profiles/r06/slow/).  The loser is probed again after kTuneReprobe launches,
+// and each probe that confirms the choice doubles that interval (up to
+// kTuneReprobeMax), so a settled choice costs few probe launches.
 // The line-aligned class keeps its cap unmeasured: it won 4-9 % on every box.
 // Launches below kTuneMinBytes use the current choice; an explicit
 // s3dg_set_occupancy / s3dg_set_batch_pace (or S3DG_ZC_TUNE=0) turns the
 // check off.
 constexpr uint64_t kTuneMinBytes = 1ull << 30;
-constexpr uint64_t kTuneReprobe = 32;
+constexpr uint64_t kTuneReprobe = 32, kTuneReprobeMax = 1024;
 constexpr int kTuneKeep = 5, kTuneFirst = 4;
 constexpr double kTuneMargin = 0.01;
 struct ZcTuner {
     int best = 0;                  // 0 = the fitted rule, 1 = uncapped, no floor
     uint64_t launches = 0;         // timed launches issued
     uint64_t issued[2] = {0, 0};
+    uint64_t interval = kTuneReprobe;   // launches between probes of the loser
+    uint64_t next_probe = 0;            // launch index of the next probe (0: not scheduled)
+    bool warm = false;                  // the first timed launch has been dropped
     double recent[2][kTuneKeep] = {};   // GB/s of the last kTuneKeep timed launches of each
     int samples[2] = {0, 0};
     struct Pending {
@@ -331,14 +340,13 @@ bool tune_enabled() {
     return on;
 }
 
-// Median rate (GB/s) of candidate q's last kTuneKeep timed launches (0: none).
-double tune_median(const ZcTuner &T, int q) {
+// Mean rate (GB/s) of candidate q's last kTuneKeep timed launches (0: none).
+double tune_mean(const ZcTuner &T, int q) {
     const int n = std::min(T.samples[q], kTuneKeep);
     if (n == 0) return 0.0;
-    double v[kTuneKeep];
-    std::copy(T.recent[q], T.recent[q] + n, v);
-    std::sort(v, v + n);
-    return n & 1 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
+    double sum = 0.0;
+    for (int k = 0; k < n; ++k) sum += T.recent[q][k];
+    return sum / n;
 }
 
 // A launch of class zc writing `bytes`: the candidate to run (0 = the fitted
@@ -349,6 +357,7 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
     std::lock_guard<std::mutex> g(c->mu);
     ZcTuner &T = c->tune[zc];
     // harvest finished measurements (never waits)
+    int probed = 0;   // new samples of the candidate not chosen
     for (size_t k = 0; k < T.pend.size();) {
         ZcTuner::Pending &p = T.pend[k];
         if (hipEventQuery(p.b) != hipSuccess) {
@@ -358,8 +367,13 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
         }
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess && ms > 0.f) {
-            T.recent[p.cand][T.samples[p.cand] % kTuneKeep] = p.bytes / (ms * 1e6);
-            ++T.samples[p.cand];
+            if (!T.warm) {
+                T.warm = true;   // the context's first timed launch: warm-up, not a sample
+            } else {
+                T.recent[p.cand][T.samples[p.cand] % kTuneKeep] = p.bytes / (ms * 1e6);
+                ++T.samples[p.cand];
+                if (p.cand != T.best) ++probed;
+            }
         }
         (void)hipGetLastError();
         T.spare.push_back(p.a);
@@ -368,14 +382,27 @@ int tune_pick(s3dg_ctx *c, int zc, uint64_t bytes, bool *timed, ZcTuner::Pending
         T.pend.pop_back();
     }
     if (T.samples[0] >= kTuneFirst && T.samples[1] >= kTuneFirst) {
-        const double med[2] = {tune_median(T, 0), tune_median(T, 1)};
+        const double mean[2] = {tune_mean(T, 0), tune_mean(T, 1)};
         // switch only when the other candidate is clearly faster (hysteresis)
-        if (med[1 - T.best] > med[T.best] * (1.0 + kTuneMargin)) T.best = 1 - T.best;
+        if (mean[1 - T.best] > mean[T.best] * (1.0 + kTuneMargin)) {
+            T.best = 1 - T.best;
+            T.interval = kTuneReprobe;
+        } else if (probed) {   // a probe confirmed the choice: probe less often
+            T.interval = std::min(2 * T.interval, kTuneReprobeMax);
+        }
     }
     if (bytes < kTuneMinBytes) return T.best;
-    const int cand = T.issued[0] < (uint64_t)kTuneFirst || T.issued[1] < (uint64_t)kTuneFirst
-                         ? (int)(T.launches & 1)                                 // rule, plain, rule, plain
-                     : (T.launches % kTuneReprobe == kTuneReprobe - 1) ? 1 - T.best : T.best;
+    int cand;
+    if (T.issued[0] < (uint64_t)kTuneFirst + 1 || T.issued[1] < (uint64_t)kTuneFirst) {
+        cand = (int)(T.launches & 1);   // rule, plain, rule, plain (the first launch is the warm-up)
+    } else {
+        if (T.next_probe == 0) T.next_probe = T.launches + T.interval;
+        cand = T.best;
+        if (T.launches >= T.next_probe) {
+            cand = 1 - T.best;
+            T.next_probe = T.launches + T.interval;
+        }
+    }
     if (T.pend.size() < 16) {
         for (int q = 0; q < 2; ++q) {
             hipEvent_t &e = q ? probe->b : probe->a;
@@ -705,8 +732,8 @@ int s3dg_query_zero_tune(s3dg_ctx *c, int zclass, int *best, double *rule_gbs, d
     std::lock_guard<std::mutex> g(c->mu);
     const ZcTuner &T = c->tune[zclass];
     if (best) *best = T.best;
-    if (rule_gbs) *rule_gbs = tune_median(T, 0);
-    if (plain_gbs) *plain_gbs = tune_median(T, 1);
+    if (rule_gbs) *rule_gbs = tune_mean(T, 0);
+    if (plain_gbs) *plain_gbs = tune_mean(T, 1);
     if (timed) *timed = T.launches;
     return S3DG_OK;
 }
