@@ -576,7 +576,7 @@ def main() -> int:
                     "kernel": kernel, "launch_shape": launch_shape,
                     "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": algo_per_launch,
-                    "launch_ms_distribution": launch_distribution(kern_ms, launch_bytes),
+                    "launch_ms_distribution": launch_distribution(kern_ms, launch_bytes, len(launches)),
                     "source_digest": src_digest, "library_digest": lib_digest}
         if kind in ("stream", "batch"):
             # the zero-class setting the context measured and chose (s3dg_query_zero_tune)
@@ -637,7 +637,7 @@ def even_ring(n: int, cap_objs: int) -> int:
     return -(-n // passes)
 
 
-def launch_distribution(ms: list, nbytes: list) -> dict:
+def launch_distribution(ms: list, nbytes: list, per_step: int = 1) -> dict:
     """Per-launch HIP-event times of the timed steps (the mean is
     what the line scores, and a bimodal run shows here): mean, p10/p50/p90,
     max, and per-launch rates (per byte, so launches of
@@ -657,6 +657,12 @@ def launch_distribution(ms: list, nbytes: list) -> dict:
         out.update({"GBps_min": round(rates[0], 1), "GBps_p10": round(pct(rates, 0.1), 1),
                     "GBps_p50": round(pct(rates, 0.5), 1), "GBps_p90": round(fast, 1),
                     "slow_share_rate_below_p90_over_1.06": round(sum(r < fast / 1.06 for r in rates) / len(rates), 4)})
+        # where the slow launches sit: their indices in the timed sequence
+        # (launch k is step k // per_step, position k % per_step)
+        slow = [k for k, (m, b) in enumerate(zip(ms, nbytes)) if m > 0 and b / (m * 1e6) < fast / 1.06]
+        out["slow_launch_indices"] = slow[:64]
+        if per_step > 1:
+            out["slow_by_position_in_step"] = [sum(1 for k in slow if k % per_step == q) for q in range(per_step)]
     return out
 
 
