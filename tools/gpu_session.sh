@@ -67,10 +67,13 @@ for step in "$@"; do
             -- python3 bench.py --config "$a" --steps 3 --warmup 1 --no-ceiling --no-d2h --no-cpu-baseline \
             --no-verify > "$OUT/$tag.log" 2>&1; rc=$?
         tail -1 "$OUT/$tag.log";;
-    pmcx)           # per-XCC counters (tools/xcc_counters.yaml) over a lab script: pmcx:SCRIPT:C1,C2,...
+    pmcx)           # per-XCC counters (tools/xcc_counters.yaml) over a lab script: pmcx:SCRIPT:C1,C2,...[:ENV]
         ctrs=$(echo "$b" | tr ',' ' ')
+        envs=$(echo "$c" | tr ',' ' ')
+        for e in $envs; do export "$e"; done
         timeout -s KILL 120 rocprofv3 -E tools/xcc_counters.yaml --pmc $ctrs -d "$OUT/$tag" -o run \
             --output-format csv -- python3 "tools/$a" > "$OUT/$tag.log" 2>&1; rc=$?
+        for e in $envs; do unset "${e%%=*}"; done
         tail -1 "$OUT/$tag.log";;
     exe)            # a native program built here (e.g. tools/_native/dispatch_lab)
         timeout -k 10 300 "$a" > "$OUT/$tag.log" 2>&1; rc=$?

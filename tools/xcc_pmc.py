@@ -45,6 +45,16 @@ def main():
         for j in range(2):
             call("s3dg_dgen_fill", ctx._h, p + j * 8 * GiB, 8 * GiB, 0, 1 << 40, 1, 0, 1,
                  object_entropy(sb, j), sh)
+    if os.environ.get("LAB_KIND") == "cfg5":
+        # config 5's launch shape (d2 c3) with the store floor forced to
+        # LAB_PACE ticks (0: plain): LAB_N launches, to compare the counters
+        # of the slow launches (12.1-12.8 ms) with the fast ones (11.0-11.3)
+        ctx.set_batch_pace(int(os.environ.get("LAB_PACE", "0")))
+        for k in range(int(os.environ.get("LAB_N", "16"))):
+            call("s3dg_fill_controlled_stream", ctx._h, p, size, size, n, 2, 2, 3, sb, 0, sh)
+            torch.cuda.synchronize()
+        print("xcc_pmc ok", flush=True)
+        return
     if os.environ.get("LAB_SMI") == "1":
         return smi_mode(torch, {"fill": (fill, n * size), "k2": (k2, n * size), "dg1": (dg1, 16 * GiB)})
     for r in range(int(os.environ.get("LAB_ROUNDS", "2"))):
