@@ -160,6 +160,8 @@ def parse():
     p.add_argument("--cpu-no-pin", action="store_true",
                    help="leave the CPU baseline's threads to the scheduler (default: bound to the cgroup's share of "
                         "CPUs, GPU-local and idlest first)")
+    p.add_argument("--legacy-stream", action="store_true",
+                   help="launch on torch's default (legacy null) stream, as rounds 1-5 did")
     p.add_argument("--no-d2h", action="store_true")
     p.add_argument("--d2h-reps", type=int, default=1, help="D2H-inclusive samples (diagnosis of run-to-run spread)")
     p.add_argument("--d2h-full", action="store_true",
@@ -272,7 +274,8 @@ def main() -> int:
     # every launch on a (non-blocking) stream of torch's pool, not the legacy
     # default stream, whose launches HIP orders against every blocking stream
     # (the single-call configs 11-13 paid ~0.8 us per call for it)
-    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+    if not args.legacy_stream:
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     fn, fd = compress_ratio(cfg["compress"])
