@@ -998,9 +998,10 @@ def cpu_idle_fractions(window: float = 0.25) -> dict:
 
 def pin_cpus(dev: int, n: int) -> list[int]:
     """n CPUs of this process's affinity: those on the GPU's NUMA node first,
-    and within each group the ones idlest right now (/proc/stat over 0.25 s),
-    so a baseline pinned on a shared host does not land on CPUs other jobs
-    are busy on (VERDICT r05 next #6)."""
+    one per physical core, the cores idlest right now first (/proc/stat over
+    0.25 s, a core as idle as its busiest hardware thread), so a baseline
+    pinned on a shared host does not land on cores other jobs are busy on
+    (VERDICT r05 next #6)."""
     aff = sorted(os.sched_getaffinity(0))
     local = []
     try:
@@ -1016,8 +1017,32 @@ def pin_cpus(dev: int, n: int) -> list[int]:
     except Exception:
         local = []
     idle = cpu_idle_fractions()
-    key = lambda c: -idle.get(c, 0.0)  # noqa: E731
-    return (sorted(local, key=key) + sorted((c for c in aff if c not in local), key=key))[:n]
+
+    def siblings(c):
+        try:
+            out = set()
+            for part in open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip().split(","):
+                a, _, b = part.partition("-")
+                out.update(range(int(a), int(b or a) + 1))
+            return out
+        except Exception:
+            return {c}
+    # one logical CPU per physical core, the cores whose every hardware thread
+    # is idle first: an "idle" CPU whose SMT sibling runs another job's thread
+    # gives a baseline thread half a core (round 6's first pinned lines ran
+    # 30-50 % below the unpinned samples beside them)
+    def core_score(c):
+        return min(idle.get(x, 0.0) for x in siblings(c))
+    picked, used = [], set()
+    for group in (local, [c for c in aff if c not in local]):
+        for c in sorted(group, key=lambda c: (-core_score(c), c)):
+            if c in used:
+                continue
+            picked.append(c)
+            used |= siblings(c)
+    if len(picked) < n:   # fewer cores than threads: add second hardware threads
+        picked += [c for c in sorted(aff, key=lambda c: -idle.get(c, 0.0)) if c not in picked]
+    return picked[:n]
 
 
 def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=True):
