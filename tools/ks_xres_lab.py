@@ -120,6 +120,31 @@ def main():
                 if rnd:
                     acc.setdefault(name, []).append(gbs)
     os.environ.pop("S3DG_KS_XRES", None)
+    # DG1 per-object launches (config 14's shape): lane length alone (the
+    # copy's mode-1 lanes at 512 draws, product order), 8 GiB objects
+    assert libs["lab"].s3dg_set_keystream_shape(ctx["lab"], 1, 0, 0, 0, u64(512), -1) == 0
+    obj = 8 << 30
+    from s3dlio_amd import object_entropy
+
+    def dg1(k, j):
+        assert libs[k].s3dg_dgen_fill(ctx[k], ctypes.c_void_p(buf.data_ptr() + (j % 8) * obj), u64(obj), u64(0),
+                                      u64(1 << 40), u64(1), ctypes.c_uint32(0), ctypes.c_uint32(1),
+                                      u64(object_entropy(0x5EED000000000001, j)), sh) == 0
+    with torch.cuda.stream(st):
+        for rnd in range(int(os.environ.get("LAB_ROUNDS", "4"))):
+            for name in ("product", "lab"):
+                dg1(name, 0)
+                st.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for j in range(10):
+                    dg1(name, j)
+                e1.record(st)
+                e1.synchronize()
+                gbs = 10 * obj / (e0.elapsed_time(e1) * 1e6)
+                print(json.dumps({"round": rnd, "case": "dg1_8g_" + name, "GBps": round(gbs, 1)}), flush=True)
+                if rnd:
+                    acc.setdefault("dg1_8g_" + name, []).append(gbs)
     for name, v in acc.items():
         print(json.dumps({"summary": name, "GBps_mean": round(sum(v) / len(v), 1), "rounds": len(v)}), flush=True)
     print("ks_xres_lab ok", flush=True)
