@@ -527,10 +527,11 @@ uint8_t *user_registered(const uint8_t *p, uint64_t n, bool direct_ok, UserHold 
     if (it != R.regs.begin()) {
         --it;
         if (a >= it->first && a + n <= it->first + it->second.bytes) {
-            if (!direct_ok) return nullptr;   // inside: the regular paths' copies are valid too
+            // inside: held until the call returns, direct or not (a copy-engine
+            // copy into it must not see the pages unregistered mid-flight)
             ++it->second.users;
             hold.key = it->first;
-            return it->second.dev + (a - it->first);
+            return direct_ok ? it->second.dev + (a - it->first) : nullptr;
         }
     }
     const uintptr_t lo = a & ~(uintptr_t)4095, hi = (a + n + 4095) & ~(uintptr_t)4095;
