@@ -279,7 +279,8 @@ int s3dg_host_free_pinned(void *p);
  * its pages and the next call into it is a GPU memory fault.  The bindings
  * hold the buffer for the registration's lifetime (Python:
  * s3dlio_amd.register_host_buffer keeps an export of it; Rust:
- * HostRegistration<'a> borrows the slice).
+ * HostRegistration<'a> borrows the slice).  Register a range
+ * while no other thread's call is writing into it.
  * Replaces round 5's S3DLIO_HOST_REGISTER=1 sighting rule, which registered
  * buffers their owners did not know about. */
 int s3dg_host_register(void *buf, uint64_t len);
