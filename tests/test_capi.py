@@ -82,6 +82,26 @@ def test_no_gpu_is_an_error_not_a_fallback():
         S.fill_controlled_data(bytearray(4096), 1, 1)
 
 
+def test_registration_handle_without_gpu():
+    """register_host_buffer (s3dg_host_register behind a handle that holds the
+    buffer while registered): without a GPU the call raises and
+    the handle lets go of the buffer (it can be resized again); an empty buffer
+    needs no call; read-only buffers are refused before any call."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import s3dlio_amd as S
+    b = bytearray(8192)
+    with pytest.raises(RuntimeError, match="hipHostRegister"):
+        S.register_host_buffer(b)
+    b.extend(b"x")                       # no export left behind
+    with S.register_host_buffer(bytearray(0)) as h:
+        assert h.nbytes == 0
+    with pytest.raises(ValueError, match="writable"):
+        S.register_host_buffer(b"\x00" * 16)
+    assert S.unregister_host_buffer() == 0
+
+
 def test_buffer_argument_errors():
     import s3dlio_amd as S
     with pytest.raises(ValueError, match="writable"):
