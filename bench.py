@@ -996,7 +996,7 @@ def cpu_idle_fractions(window: float = 0.25) -> dict:
     return {c: (b[c][0] - a[c][0]) / max(1, b[c][1] - a[c][1]) for c in a if c in b}
 
 
-def pin_cpus(dev: int, n: int) -> list[int]:
+def pin_cpus(dev: int, n: int, policy: str = "local") -> list[int]:
     """n CPUs of this process's affinity: those on the GPU's NUMA node first,
     one per physical core, the cores idlest right now first (/proc/stat over
     0.25 s, a core as idle as its busiest hardware thread), so a baseline
@@ -1005,6 +1005,8 @@ def pin_cpus(dev: int, n: int) -> list[int]:
     aff = sorted(os.sched_getaffinity(0))
     local = []
     try:
+        if policy != "local":
+            raise LookupError("no node preference")
         from s3dlio_amd._lib import lib
         node = ctypes.c_int(-1)
         lib.s3dg_device_numa_node(dev, ctypes.byref(node))
@@ -1057,7 +1059,7 @@ def cpu_baseline(cfg, fn, fd, seconds, sizes, dev=0, reps=7, pin=True):
     the affinity list and its samples spread 10-400 % on the shared 256-CPU
     host (profiles/r04/bench/d_*), where others' jobs ran on them."""
     share = cpu_share()
-    cpus = pin_cpus(dev, share["threads"]) if pin else None
+    cpus = pin_cpus(dev, share["threads"], os.environ.get("S3DG_CPU_PIN_POLICY", "local")) if pin else None
     saved = os.sched_getaffinity(0)
     runs = []
     try:
