@@ -998,11 +998,11 @@ def cpu_idle_fractions(window: float = 0.25) -> dict:
 
 def pin_cpus(dev: int, n: int, policy: str = "local") -> list[int]:
     """n CPUs of this process's affinity: those on the GPU's NUMA node first,
-    one per physical core, dealt round-robin over the L3 domains (CCDs), the
-    cores idlest right now first within each (/proc/stat over 0.25 s, a core
-    as idle as its busiest hardware thread), so a baseline pinned on a shared
+    one per physical core, up to S3DG_CPU_PER_CCD (4) from each L3 domain
+    (CCD), the idlest CCDs and cores first (/proc/stat over 0.25 s, a core as
+    idle as its busiest hardware thread), so a baseline pinned on a shared
     host neither lands on cores other jobs are busy on nor packs its threads
-    onto a few CCDs' memory links (VERDICT r05 next #6)."""
+    onto one or two CCDs' memory links (VERDICT r05 next #6)."""
     aff = sorted(os.sched_getaffinity(0))
     local = []
     try:
@@ -1036,29 +1036,35 @@ def pin_cpus(dev: int, n: int, policy: str = "local") -> list[int]:
     # 30-50 % below the unpinned samples beside them)
     def core_score(c):
         return min(idle.get(x, 0.0) for x in siblings(c))
-    # ... spread round-robin over the L3 domains (CCDs): a CCD's link to
-    # memory carries ~60 GB/s, so 16 threads packed on two CCDs wrote 85 GiB/s
-    # where the same count spread by the scheduler wrote 150 (round 6,
-    # profiles/r06/cpu/)
+    # ... by L3 domain (CCD): a CCD's link to memory carries ~60 GB/s, so 16
+    # threads packed on two CCDs wrote 85 GiB/s where the same count spread by
+    # the scheduler wrote 150 (round 6, profiles/r06/cpu/)
     def l3(c):
         try:
             return open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read().strip()
         except Exception:
             return "?"
+    # whole CCDs when they are idle: the idlest L3 domains first, up to
+    # per_dom cores from each (one CCD link ~60 GB/s: four CCDs carry the
+    # port's ~150 GiB/s, and a CCD no other job runs on keeps the samples
+    # tight; spreading one core over every CCD shared each with other jobs)
+    per_dom = int(os.environ.get("S3DG_CPU_PER_CCD", "4"))
     picked, used = [], set()
     for group in (local, [c for c in aff if c not in local]):
         doms = {}
         for c in sorted(group, key=lambda c: (-core_score(c), c)):
             doms.setdefault(l3(c), []).append(c)
-        queues = list(doms.values())
-        while any(queues):
-            for q in queues:
-                while q and q[0] in used:
-                    q.pop(0)
-                if q:
-                    c = q.pop(0)
-                    picked.append(c)
-                    used |= siblings(c)
+        order = sorted(doms.values(), key=lambda q: -sum(core_score(c) for c in q) / max(1, len(q)))
+        for q in order:
+            took = 0
+            for c in q:
+                if took >= per_dom or len(picked) >= n:
+                    break
+                if c in used:
+                    continue
+                picked.append(c)
+                used |= siblings(c)
+                took += 1
     if len(picked) < n:   # fewer cores than threads: add second hardware threads
         picked += [c for c in sorted(aff, key=lambda c: -idle.get(c, 0.0)) if c not in picked]
     return picked[:n]
