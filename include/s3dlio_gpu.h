@@ -174,14 +174,16 @@ int s3dg_compress_ratio(uint64_t compress, uint32_t *f_num, uint32_t *f_den);
 int s3dg_zero_class(uint32_t f_num, uint32_t f_den);
 /* Batch-kernel launches of zero class 2 (above) check their store floor by
  * measurement: the context times its own launches of >= 1 GiB and runs the
- * floor or a plain launch (medians of each one's last five rates, after four
- * launches of each; the other is taken only when more than 1 % faster than
- * the current choice, so near-equal candidates do not flip between runs),
- * re-probing the other every 32 launches; class 1 keeps its cap.  An
- * explicit s3dg_set_occupancy / s3dg_set_batch_pace (or env S3DG_ZC_TUNE=0)
- * turns this off.  Query (zclass 0-2): the choice (0 = the class setting, 1 =
- * plain), each one's median recent GB/s (0 = not measured yet) and the timed
- * launch count.  Results are identical. */
+ * floor or a plain launch (the means of each one's last five rates, after
+ * four launches of each, the context's first timed launch not counted; the
+ * other is taken only when more than 1 % faster than the current choice, so
+ * near-equal candidates do not flip between runs), re-probing the other after
+ * 32 launches, an interval that doubles with every probe that confirms the
+ * choice (up to 1024); class 1 keeps its cap.  An explicit
+ * s3dg_set_occupancy / s3dg_set_batch_pace (or env S3DG_ZC_TUNE=0) turns this
+ * off.  Query (zclass 0-2): the choice (0 = the class setting, 1 = plain),
+ * each one's mean recent GB/s (0 = not measured yet) and the timed launch
+ * count.  Results are identical. */
 int s3dg_query_zero_tune(s3dg_ctx *ctx, int zclass, int *best, double *rule_gbs, double *plain_gbs,
                          uint64_t *timed);
 /* Per-object entropy of object j of a stream: seed_base + j * 2^32. */
