@@ -8,7 +8,7 @@ from a diagnostic build with the Xoshiro steps replaced by adds
 design), blocks of LAB_REPS launches alternating, with the amdsmi GFX clock
 and socket power polled every ~5 ms.  Also the fill (config 2) for reference.
 
-    python tools/ks_power_lab.py --build     # here: tools/_lab/libks_ablate32.so
+    python tools/ks_power_lab.py --build     # here: tools/_labso/libks_ablate32.so
     python tools/ks_power_lab.py             # GPU box
 Tooling only: nothing in the product imports this."""
 import ctypes
@@ -22,7 +22,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-OUT = os.path.join(ROOT, "tools", "_lab")
+OUT = os.path.join(ROOT, "tools", "_labso")
 MiB = 1 << 20
 
 
