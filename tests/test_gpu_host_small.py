@@ -312,7 +312,9 @@ def test_registered_buffer_remapped_child(oracle, golden_base):
     mapping goes with the pages and the next store faults, measured in round
     6; no test does that.)  Then the Python binding: a bytearray loop whose
     registration handle holds the buffer (it cannot be resized or freed while
-    registered) and releases it at the end of the `with` block."""
+    registered) and releases it at the end of the `with` block; and a handle
+    whose pages a newer handle's registration took over leaves that
+    registration in place when it closes."""
     code = (
         "import ctypes, numpy as np, sys; sys.path.insert(0, %r)\n"
         "import s3dlio_amd as S\n"
@@ -355,6 +357,14 @@ def test_registered_buffer_remapped_child(oracle, golden_base):
         "    b.extend(b'x')   # released: the buffer is the caller's again\n"
         "    del b\n"
         "assert L.s3dg_host_unregister(None) == 0\n"
+        "b = bytearray(2 * MiB)\n"
+        "h1 = S.register_host_buffer(memoryview(b)[:MiB])\n"
+        "h2 = S.register_host_buffer(memoryview(b))   # takes over h1's pages\n"
+        "h1.close()                                   # must leave h2's registration\n"
+        "S.fill_controlled_data_seeded(memoryview(b), 1, 2, 60, gb.tobytes())\n"
+        "assert bytes(b) == bytes(OC.fill_controlled(2 * MiB, 1, 1, 2, 60, gb))\n"
+        "n = L.s3dg_host_unregister(None); assert n == 1, n\n"
+        "h2.close(); del h1, h2; b.extend(b'x')\n"
         "print('remapped ok')\n" % (ROOT, os.path.join(ROOT, "tests", "golden", "base_block_ba5eb10c.bin")))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
