@@ -40,6 +40,7 @@ import hashlib
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -837,6 +838,22 @@ def traffic_from_profiles(config: int, launch_bytes: int):
     return None
 
 
+def pcie_link(torch, dev: int):
+    """The GPU function's PCIe link and its upstream port's, as sysfs reports
+    them ("32.0 GT/s PCIe x16"), or None where unreadable."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+        p = os.path.realpath(f"/sys/bus/pci/devices/{bdf}")
+        out = []
+        for d in (p, os.path.dirname(p)):
+            with open(d + "/current_link_speed") as f, open(d + "/current_link_width") as g:
+                out.append(f"{f.read().strip()} x{g.read().strip()}")
+        return out
+    except Exception:
+        return None
+
+
 def numa_of(ptr: int) -> dict:
     """NUMA placement of the mapping holding `ptr` (/proc/self/numa_maps:
     pages per node of the mapping that starts at or below ptr)."""
@@ -931,8 +948,10 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
         # the first GiBs into fresh pinned pages copy slower
         run(max(2, nchunks // 4) if n_objs is None else min(4, nchunks), False)
         torch.cuda.synchronize()
+        link_before = pcie_link(torch, dev)
         t0 = time.perf_counter()
         run(nchunks, True)
+        link_during = pcie_link(torch, dev)   # read while the last copies run
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         pages = [numa_of(p) for p in host]
@@ -950,7 +969,8 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
         for p in host:
             call("s3dg_host_free_pinned", p)
     done_bytes = sum(chunk_bytes(k) for k in range(nchunks))
-    rates = sorted(chunk_bytes(k) / (a.elapsed_time(b) * 1e-3) / GiB for k, (a, b) in enumerate(cev))
+    seq = [chunk_bytes(k) / (a.elapsed_time(b) * 1e-3) / GiB for k, (a, b) in enumerate(cev)]
+    rates = sorted(seq)
     cpus = sorted(os.sched_getaffinity(0))
     cpu_nodes = set()
     for nd in os.listdir("/sys/devices/system/node") if os.path.isdir("/sys/devices/system/node") else []:
@@ -974,8 +994,14 @@ def d2h_inclusive(torch, ctx, call, dev, cfg, fn, fd, lo, total=8 * GiB, chunk=2
            "sample": f"{what}, 2 device chunks of {cb // MiB} MiB, pinned host ring (hipHostMalloc default flags, "
                      f"allocated from a thread bound to the GPU's local CPUs), generate || D2H on two streams",
            "gpu_numa_node": node.value, "ring_pages_per_node": pages,
+           "pcie_link_gpu_upstream": {"before": link_before, "end": link_during},
            "process_cpu_nodes": sorted(cpu_nodes),
-           "copy_GiBps_min_med_max": [round(rates[0], 1), round(rates[len(rates) // 2], 1), round(rates[-1], 1)]}
+           "copy_GiBps_min_med_max": [round(rates[0], 1), round(rates[len(rates) // 2], 1), round(rates[-1], 1)],
+           # per host slot (copy k lands in slot k % 2), and the timed copies
+           # below 3/4 of the best slot's median, by position (0 = first timed copy)
+           "copy_GiBps_med_by_slot": [round(statistics.median(seq[s::2]), 1) for s in range(2) if seq[s::2]],
+           "slow_copies": [[k, round(r, 1)] for k, r in enumerate(seq)
+                           if r < 0.75 * max(statistics.median(seq[s::2]) for s in range(2) if seq[s::2])][:16]}
     if n_objs is not None:
         out["verified_vs_oracle"] = verified
     return out
