@@ -44,3 +44,16 @@ def test_pin_cpus_within_affinity_one_per_core():
     assert len(cpus) == n and len(set(cpus)) == n and set(cpus) <= set(aff)
     for policy in ("local", "any"):
         assert set(bench.pin_cpus(0, n, policy)) <= set(aff)
+
+
+def test_pcie_link_without_a_gpu_is_none():
+    """The D2H sample's link probe never raises: no GPU (or no sysfs) -> None."""
+    import torch
+    assert bench.pcie_link(torch, 0) is None or all(isinstance(s, str) for s in bench.pcie_link(torch, 0))
+
+    class NoCuda:
+        class cuda:
+            @staticmethod
+            def get_device_properties(dev):
+                raise RuntimeError("no GPU")
+    assert bench.pcie_link(NoCuda, 0) is None
